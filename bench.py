@@ -1,0 +1,233 @@
+#!/usr/bin/env python3
+"""Benchmark of the forward-encryption hot path (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1], "config 2"): one 256 MiB fp32 tensor [65536, 1024], N(0,1),
+seed = rank, resident in HBM. One STEP = encrypt + decrypt of the whole tensor, i.e.
+ConvertToFixedPoint (fp32 -> int64 mantissa + int64 exponent) followed by FixedPointToFloatPoint
+(back to fp32), both through libefl_hip.so's C ABI (efls-train/cc/efl/math/fixed_point.cc).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+value = (N x 0.25 GiB) / (max over ranks of the time of K steps / K)        [GiB/s, weak scaling]
+Multi-GPU: every rank owns its own 256 MiB shard (the path is element-wise: no payload exchange);
+the only collective is the RCCL broadcast of the 32-byte key seed from rank 0 (timed apart).
+
+roofline: per-kernel average durations come from HIP events recorded around every launch on the
+stream the kernels run on, inside the timed region. Algorithmic bytes: 20 B/element per kernel
+(encode: 4 read + 16 written; decode: 16 read + 4 written), SURVEY.md §8(d).
+cpu_baseline: the reference CPU op restated (oracle/: encode loop + GMP mpf decode, TF-Shard-like
+contiguous blocks over host threads) timed on this box on the same tensor (rank 0, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "elastic-federated-learning-solution_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "GiB/s device-resident encrypt+decrypt, 256 MiB fp32 tensor, 1/2/4/8 GPUs"
+PEAK_HBM_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+ROWS, COLS = 65536, 1024       # 256 MiB fp32
+BYTES_PER_ELEM_KERNEL = 20     # each of encode / decode
+GIB = float(1 << 30)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-threads", type=int, default=int(os.environ.get("EFL_BENCH_CPU_THREADS", "16")))
+    p.add_argument("--tune", default=os.environ.get("EFL_FXP_TUNE", ""),
+                   help="comma list kind=value for efl_fxp_tune (variant exploration)")
+    p.add_argument("--rows", type=int, default=ROWS)
+    return p.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def broadcast_seed(world, rank, dev):
+    """RCCL broadcast of the 32-byte key seed over xGMI (the path's only collective)."""
+    seed = torch.zeros(32, dtype=torch.uint8, device=dev)
+    if rank == 0:
+        seed.copy_(torch.from_numpy(np.frombuffer(os.urandom(32), np.uint8).copy()))
+    if world == 1:
+        return seed, 0.0
+    dist.broadcast(seed, 0)                     # warm the communicator
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(10):
+        dist.broadcast(seed, 0)
+    torch.cuda.synchronize()
+    return seed, (time.perf_counter() - t0) / 10 * 1e6
+
+
+def load_traffic():
+    """Per-launch HBM bytes from the rocprofv3 PMC passes (tools/pmc_traffic.py), if recorded."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(x_dev, threads):
+    from oracle import fxp
+    x = x_dev.cpu().numpy().reshape(-1)
+    fxp.baseline_encode_decode(x[: 1 << 20], threads)          # warm
+    times = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        fxp.baseline_encode_decode(x, threads)
+        times.append(time.perf_counter() - t0)
+    t = float(np.median(times))
+    return {"value": round(x.nbytes / GIB / t, 4), "unit": "GiB/s", "cores": threads,
+            "kind": "port",
+            "sample": f"whole 256 MiB tensor ({x.size} fp32), encode loop + GMP mpf decode "
+                      f"(fixed_point.cc:107-137, :235-248), {threads} threads, median of 3",
+            "ms_per_step": round(t * 1e3, 2)}
+
+
+def main():
+    args = parse()
+    world, rank, local = setup_dist(args)
+    import efl
+    dev = efl.lib.require_gpu()
+    lib = efl.lib.raw()
+    for kv in filter(None, args.tune.split(",")):
+        k, v = (int(s) for s in kv.split("="))
+        efl.lib.check(min(0, lib.efl_fxp_tune(k, v)))
+
+    seed, bcast_us = broadcast_seed(world, rank, dev)
+    n = args.rows * COLS
+    g = torch.Generator(device=dev).manual_seed(rank)
+    x = torch.randn(args.rows, COLS, device=dev, generator=g)
+    M = torch.empty(x.shape, dtype=torch.int64, device=dev)
+    E = torch.empty(x.shape, dtype=torch.int64, device=dev)
+    y = torch.empty_like(x)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+
+    def step(ev0=None, ev1=None, ev2=None):
+        if ev0 is not None:
+            ev0.record(stream)
+        efl.lib.check(lib.efl_fxp_encode(x.data_ptr(), 1, M.data_ptr(), E.data_ptr(), n, 0, sh))
+        if ev1 is not None:
+            ev1.record(stream)
+        efl.lib.check(lib.efl_fxp_decode(M.data_ptr(), E.data_ptr(), y.data_ptr(), 1, n, n, 0, sh))
+        if ev2 is not None:
+            ev2.record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # correctness gate before timing: round trip must be the identity on non-zero values
+    nz = x != 0
+    if not torch.equal(y[nz], x[nz]):
+        raise SystemExit("bench: encode/decode round trip is wrong")
+
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(*evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t_enc = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))   # ms
+    t_dec = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    if world > 1:
+        tt = torch.tensor([elapsed, t_enc, t_dec], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed, t_enc, t_dec = tt.tolist()
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = world * (n * 4) / GIB / (elapsed / args.steps)
+
+    # practical peak: device-to-device copy of the same byte volume as one kernel
+    buf_a = torch.empty(n * 5 // 4, dtype=torch.float64, device=dev) if rank == 0 else None
+    copy_gbs = None
+    if rank == 0:
+        buf_b = torch.empty_like(buf_a)
+        for _ in range(3):
+            buf_b.copy_(buf_a)
+        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        c0.record(stream)
+        for _ in range(10):
+            buf_b.copy_(buf_a)
+        c1.record(stream)
+        torch.cuda.synchronize()
+        copy_gbs = 2 * buf_a.numel() * 8 / (c0.elapsed_time(c1) / 10 * 1e-3) / 1e9
+        del buf_a, buf_b
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    dominant = "encode" if t_enc >= t_dec else "decode"
+    t_dom = max(t_enc, t_dec) * 1e-3
+    achieved = BYTES_PER_ELEM_KERNEL * n / t_dom / 1e9
+    traffic = None
+    tr = load_traffic()
+    if tr and tr.get("elements") == n and dominant in tr.get("kernels", {}):
+        traffic = tr["kernels"][dominant].get("hbm_bytes_per_launch")
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic: torch.randn fp32 on device, generator seed = rank",
+        "config": {"workload": "config 2: single 256 MiB fp32 tensor [65536,1024] per GPU, "
+                               "device-resident ConvertToFixedPoint + FixedPointToFloatPoint",
+                   "elements_per_gpu": n, "decrease_precision": False,
+                   "parallelism": f"element-wise shard, {world} x 256 MiB, RCCL seed broadcast"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
+                     "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
+                     "traffic": traffic, "kernel": dominant,
+                     "algorithmic_bytes_per_launch": BYTES_PER_ELEM_KERNEL * n},
+        "kernels_ms": {"encode": round(t_enc, 4), "decode": round(t_dec, 4)},
+        "step_roofline_frac": round(2 * BYTES_PER_ELEM_KERNEL * n / ((t_enc + t_dec) * 1e-3) / 1e9
+                                    / PEAK_HBM_GBS, 4),
+        "d2d_copy_GBs": round(copy_gbs, 1) if copy_gbs else None,
+        "seed_broadcast_us": round(bcast_us, 2),
+        "cpu_baseline": None,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(x, args.cpu_threads)
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

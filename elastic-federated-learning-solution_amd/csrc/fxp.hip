@@ -1,0 +1,634 @@
+// Stage F — fixed-point codec of EFLS-train's forward-encryption path, as streaming HIP kernels
+// for MI355X (gfx950).
+//
+// Reference: efls-train/cc/efl/math/fixed_point.cc
+//   encode  Convert2FixedPointOp<T>::Compute          :53-69 (int), :106-138 (float), :156-188 (double)
+//   decode  FixedPointToFloatPointOp<int64|string, T> :235-248 (GMP mpf), Input2Mpf :255-265
+//
+// Both directions are pure streams: per fp32 element encode reads 4 B and
+// writes 16 B, decode reads 16 B and writes 4 B — 40 algorithmic bytes per element for
+// encrypt+decrypt, no reuse, so the roofline is HBM bandwidth and the kernels are built to keep
+// every wave instruction a contiguous 16-B-per-lane access:
+//   * "pair" layout (default): lane i of a 64-lane wave owns elements 2i, 2i+1 of its 128-element
+//     stripe, so the int64 M/E streams (the 4x-wide side) move as one contiguous 1 KiB
+//     global_{load,store}_dwordx4 per wave instruction; the fp32 side moves as dwordx2.
+//   * "quad" layout: lane owns 4 consecutive elements: dwordx4 on the fp32 side, the int64 side as
+//     two dwordx4 per lane at a 32-B lane stride.
+// No LDS, no MFMA (there is no reuse and no contraction). Branch-free integer arithmetic on the
+// IEEE bit patterns; the decode reproduces GMP's truncating mpf_get_d exactly (see dec_bits).
+#include "common.h"
+
+#include <atomic>
+#include <type_traits>
+
+namespace efl {
+namespace {
+
+// ------------------------------------------------------------------------------------------
+// element transforms
+// ------------------------------------------------------------------------------------------
+
+// fixed_point.cc:108-136 for one fp32 bit pattern (SURVEY.md Appendix A rules A1-A6).
+__device__ __forceinline__ void enc_f32(uint32_t b, bool dp, long long& M, long long& E) {
+  int exp = (int)((b >> 23) & 0xFFu) - 150;                 // A1: unbiased, minus 23
+  int mant = (int)(b & 0x7FFFFFu) | (exp != 0 ? 0x800000 : 0);   // A3: test on shifted exp
+  if (dp) {                                                 // A4
+    mant >>= 13;
+    exp += 13;
+  }
+  // A5: r = ctz(mant); mant == 0 is the reference's UB shift, defined as M = 0, E = exp - 127.
+  const int r = mant ? __builtin_ctz((unsigned)mant) : -127;
+  mant = (int)((unsigned)mant >> (r & 31));
+  exp += r;
+  const int sm = (b >> 31) ? -mant : mant;                  // A6
+  M = (long long)sm;
+  E = (long long)exp;
+}
+
+// fixed_point.cc:158-186 for one fp64 bit pattern.
+__device__ __forceinline__ void enc_f64(unsigned long long b, bool dp, long long& M, long long& E) {
+  long long exp = (long long)((b >> 52) & 0x7FFull) - 1075;
+  long long mant = (long long)(b & 0xFFFFFFFFFFFFFull) | (exp != 0 ? 0x10000000000000ll : 0);
+  if (dp) {
+    mant >>= 42;
+    exp += 42;
+  }
+  const int r = mant ? __builtin_ctzll((unsigned long long)mant) : -1023;
+  mant = (long long)((unsigned long long)mant >> (r & 63));
+  exp += r;
+  M = (b >> 63) ? -mant : mant;
+  E = exp;
+}
+
+// GMP mpf_get_d of (-1)^s * a * 2^e with the exact value, a = |M| (fixed_point.cc:238-245:
+// mpf_set_z, mpf_mul_2exp / mpf_div_2exp are exact for one limb; mpf_get_d truncates):
+//   leading-bit position L >= 1024 -> +-inf; -1022..1023 normal (top 53 bits, truncated);
+//   -1074..-1023 denormal (truncated, sign kept); <= -1075 -> +0.0.
+__device__ __forceinline__ unsigned long long get_d_bits(unsigned long long a, bool neg, long long e) {
+  if (a == 0) return 0ull;
+  const unsigned long long sgn = neg ? 0x8000000000000000ull : 0ull;
+  const int p = 63 - __clzll((long long)a);
+  const long long ec = e > 4096 ? 4096 : (e < -8192 ? -8192 : e);
+  const long long L = p + ec;
+  if (L >= 1024) return sgn | 0x7FF0000000000000ull;
+  if (L <= -1075) return 0ull;
+  const unsigned long long m53 = p >= 52 ? (a >> (p - 52)) : (a << (52 - p));
+  unsigned long long bits;
+  if (L >= -1022)
+    bits = ((unsigned long long)(L + 1023) << 52) | (m53 & 0xFFFFFFFFFFFFFull);
+  else
+    bits = m53 >> (int)(-1022 - L);
+  return sgn | bits;
+}
+
+__device__ __forceinline__ unsigned long long dec_bits(long long M, long long E) {
+  const unsigned long long a = M < 0 ? 0ull - (unsigned long long)M : (unsigned long long)M;
+  return get_d_bits(a, M < 0, E);
+}
+
+// implicit double -> float of fixed_point.cc:245 (round to nearest even, IEEE denormals).
+// ftz: TF threadpool MXCSR FTZ|DAZ: |d| < 2^-126 - 2^-151 -> zero of d's sign.
+__device__ __forceinline__ float d2f(unsigned long long dbits, bool ftz) {
+  constexpr unsigned long long kTiny = 0x380FFFFFF0000000ull;   // 0x1.ffffffp-127
+  if (ftz && (dbits & 0x7FFFFFFFFFFFFFFFull) < kTiny)
+    return __uint_as_float((unsigned)(dbits >> 32) & 0x80000000u);
+  return (float)__longlong_as_double((long long)dbits);
+}
+
+// ------------------------------------------------------------------------------------------
+// memory helpers (NT bit 0: nontemporal loads, bit 1: nontemporal stores)
+// ------------------------------------------------------------------------------------------
+
+template <int NT, class T>
+__device__ __forceinline__ T ld(const T* p) {
+  if constexpr (NT & 1) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <int NT, class T>
+__device__ __forceinline__ void st(T* p, T v) {
+  if constexpr (NT & 2) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+// ------------------------------------------------------------------------------------------
+// per-"unit" ops. A unit is 2 (pair) or 4 (quad) consecutive elements; each op knows how to
+// load a unit, transform it and store it. `scalar` handles the ragged tail / unaligned case.
+// ------------------------------------------------------------------------------------------
+
+struct EncArgs {
+  const void* x;
+  long long* M;
+  long long* E;
+  int flag;   // decrease_precision
+};
+struct DecArgs {
+  const long long* M;
+  const long long* E;
+  void* y;
+  int flag;   // EFL_FXP_FTZ
+};
+
+struct EncF32Pair {
+  using Args = EncArgs;
+  static constexpr int kElems = 2;
+  using In = f2;
+  template <int NT> __device__ static In load(const Args& a, long long u) { return ld<NT>((const f2*)a.x + u); }
+  template <int NT> __device__ static void apply(const Args& a, long long u, In v) {
+    long long m0, e0, m1, e1;
+    enc_f32(__float_as_uint(v.x), a.flag, m0, e0);
+    enc_f32(__float_as_uint(v.y), a.flag, m1, e1);
+    st<NT>((ll2*)a.M + u, ll2{m0, m1});
+    st<NT>((ll2*)a.E + u, ll2{e0, e1});
+  }
+  __device__ static void scalar(const Args& a, long long i) {
+    long long m, e;
+    enc_f32(__float_as_uint(((const float*)a.x)[i]), a.flag, m, e);
+    a.M[i] = m;
+    a.E[i] = e;
+  }
+};
+
+struct EncF32Quad {
+  using Args = EncArgs;
+  static constexpr int kElems = 4;
+  using In = f4;
+  template <int NT> __device__ static In load(const Args& a, long long u) { return ld<NT>((const f4*)a.x + u); }
+  template <int NT> __device__ static void apply(const Args& a, long long u, In v) {
+    long long m0, e0, m1, e1, m2, e2, m3, e3;
+    enc_f32(__float_as_uint(v.x), a.flag, m0, e0);
+    enc_f32(__float_as_uint(v.y), a.flag, m1, e1);
+    enc_f32(__float_as_uint(v.z), a.flag, m2, e2);
+    enc_f32(__float_as_uint(v.w), a.flag, m3, e3);
+    st<NT>((ll2*)a.M + 2 * u, ll2{m0, m1});
+    st<NT>((ll2*)a.M + 2 * u + 1, ll2{m2, m3});
+    st<NT>((ll2*)a.E + 2 * u, ll2{e0, e1});
+    st<NT>((ll2*)a.E + 2 * u + 1, ll2{e2, e3});
+  }
+  __device__ static void scalar(const Args& a, long long i) { EncF32Pair::scalar(a, i); }
+};
+
+struct EncF64Pair {
+  using Args = EncArgs;
+  static constexpr int kElems = 2;
+  using In = ll2;
+  template <int NT> __device__ static In load(const Args& a, long long u) { return ld<NT>((const ll2*)a.x + u); }
+  template <int NT> __device__ static void apply(const Args& a, long long u, In v) {
+    long long m0, e0, m1, e1;
+    enc_f64((unsigned long long)v.x, a.flag, m0, e0);
+    enc_f64((unsigned long long)v.y, a.flag, m1, e1);
+    st<NT>((ll2*)a.M + u, ll2{m0, m1});
+    st<NT>((ll2*)a.E + u, ll2{e0, e1});
+  }
+  __device__ static void scalar(const Args& a, long long i) {
+    long long m, e;
+    enc_f64(((const unsigned long long*)a.x)[i], a.flag, m, e);
+    a.M[i] = m;
+    a.E[i] = e;
+  }
+};
+
+// Int2FixedPoint (fixed_point.cc:53-69): M = x, E = 0.
+template <class T, class V2>
+struct EncIntPair {
+  using Args = EncArgs;
+  static constexpr int kElems = 2;
+  using In = V2;
+  template <int NT> __device__ static In load(const Args& a, long long u) { return ld<NT>((const V2*)a.x + u); }
+  template <int NT> __device__ static void apply(const Args& a, long long u, In v) {
+    st<NT>((ll2*)a.M + u, ll2{(long long)v.x, (long long)v.y});
+    st<NT>((ll2*)a.E + u, ll2{0, 0});
+  }
+  __device__ static void scalar(const Args& a, long long i) {
+    a.M[i] = (long long)((const T*)a.x)[i];
+    a.E[i] = 0;
+  }
+};
+
+struct DecF32Pair {
+  using Args = DecArgs;
+  static constexpr int kElems = 2;
+  struct In { ll2 m, e; };
+  template <int NT> __device__ static In load(const Args& a, long long u) {
+    return In{ld<NT>((const ll2*)a.M + u), ld<NT>((const ll2*)a.E + u)};
+  }
+  template <int NT> __device__ static void apply(const Args& a, long long u, In v) {
+    const bool ftz = a.flag & EFL_FXP_FTZ;
+    f2 r{d2f(dec_bits(v.m.x, v.e.x), ftz), d2f(dec_bits(v.m.y, v.e.y), ftz)};
+    st<NT>((f2*)a.y + u, r);
+  }
+  __device__ static void scalar(const Args& a, long long i) {
+    ((float*)a.y)[i] = d2f(dec_bits(a.M[i], a.E[i]), a.flag & EFL_FXP_FTZ);
+  }
+};
+
+struct DecF32Quad {
+  using Args = DecArgs;
+  static constexpr int kElems = 4;
+  struct In { ll2 m0, m1, e0, e1; };
+  template <int NT> __device__ static In load(const Args& a, long long u) {
+    const ll2* M = (const ll2*)a.M + 2 * u;
+    const ll2* E = (const ll2*)a.E + 2 * u;
+    return In{ld<NT>(M), ld<NT>(M + 1), ld<NT>(E), ld<NT>(E + 1)};
+  }
+  template <int NT> __device__ static void apply(const Args& a, long long u, In v) {
+    const bool ftz = a.flag & EFL_FXP_FTZ;
+    f4 r{d2f(dec_bits(v.m0.x, v.e0.x), ftz), d2f(dec_bits(v.m0.y, v.e0.y), ftz),
+         d2f(dec_bits(v.m1.x, v.e1.x), ftz), d2f(dec_bits(v.m1.y, v.e1.y), ftz)};
+    st<NT>((f4*)a.y + u, r);
+  }
+  __device__ static void scalar(const Args& a, long long i) { DecF32Pair::scalar(a, i); }
+};
+
+struct DecF64Pair {
+  using Args = DecArgs;
+  static constexpr int kElems = 2;
+  struct In { ll2 m, e; };
+  template <int NT> __device__ static In load(const Args& a, long long u) {
+    return In{ld<NT>((const ll2*)a.M + u), ld<NT>((const ll2*)a.E + u)};
+  }
+  template <int NT> __device__ static void apply(const Args& a, long long u, In v) {
+    ll2 r{(long long)dec_bits(v.m.x, v.e.x), (long long)dec_bits(v.m.y, v.e.y)};
+    st<NT>((ll2*)a.y + u, r);
+  }
+  __device__ static void scalar(const Args& a, long long i) {
+    ((unsigned long long*)a.y)[i] = dec_bits(a.M[i], a.E[i]);
+  }
+};
+
+// ------------------------------------------------------------------------------------------
+// kernels
+// ------------------------------------------------------------------------------------------
+
+// Streaming kernel: tiles of kBlock*K units; a workgroup walks tiles blockIdx.x, +gridDim.x, ...
+// Inside a full tile every lane issues its K loads back to back before any store (K 16-B loads
+// in flight per lane), then transforms and stores. Tile t of a wave touches one contiguous span.
+template <class Op, int K, int NT>
+__global__ __launch_bounds__(kBlock) void k_stream(typename Op::Args a, long long nunits) {
+  const long long tile = (long long)kBlock * K;
+  for (long long base = (long long)blockIdx.x * tile; base < nunits;
+       base += (long long)gridDim.x * tile) {
+    typename Op::In v[K];
+    if (base + tile <= nunits) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) v[k] = Op::template load<NT>(a, base + k * kBlock + threadIdx.x);
+#pragma unroll
+      for (int k = 0; k < K; ++k) Op::template apply<NT>(a, base + k * kBlock + threadIdx.x, v[k]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const long long u = base + k * kBlock + threadIdx.x;
+        if (u < nunits) v[k] = Op::template load<NT>(a, u);
+      }
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const long long u = base + k * kBlock + threadIdx.x;
+        if (u < nunits) Op::template apply<NT>(a, u, v[k]);
+      }
+    }
+  }
+}
+
+// Element-at-a-time kernel for the ragged tail and for unaligned buffers.
+template <class Op>
+__global__ __launch_bounds__(kBlock) void k_scalar(typename Op::Args a, long long start, long long n) {
+  for (long long i = start + (long long)blockIdx.x * kBlock + threadIdx.x; i < n;
+       i += (long long)gridDim.x * kBlock)
+    Op::scalar(a, i);
+}
+
+// Batched: blockIdx.y = tensor, blockIdx.x = tile of that tensor (one launch for `count`
+// tensors; BASELINE config 3). Arrays of pointers / sizes live in device memory.
+template <class Op, int K>
+__global__ __launch_bounds__(kBlock) void k_batched(const void* const* src, void* const* dst0,
+                                                    void* const* dst1, const long long* ns,
+                                                    int flag, long long tile_base) {
+  const long long t = tile_base + blockIdx.y;
+  const long long n = ns[t];
+  typename Op::Args a;
+  if constexpr (std::is_same<typename Op::Args, EncArgs>::value) {
+    a = EncArgs{src[t], (long long*)dst0[t], (long long*)dst1[t], flag};
+  } else {
+    a = DecArgs{(const long long*)src[t], (const long long*)dst0[t], dst1[t], flag};
+  }
+  const long long tile = (long long)kBlock * K * Op::kElems;
+  const long long e0 = (long long)blockIdx.x * tile;
+  if (e0 >= n) return;
+  // 16-B alignment of this tensor's streams decides vector vs element path (uniform branch).
+  const bool vec = aligned(src[t], 16) && aligned(dst0[t], 16) && aligned(dst1[t], 16);
+  const long long nunits = n / Op::kElems;
+  const long long u0 = (long long)blockIdx.x * kBlock * K;
+  if (vec) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const long long u = u0 + k * kBlock + threadIdx.x;
+      if (u < nunits) Op::template apply<0>(a, u, Op::template load<0>(a, u));
+    }
+    // ragged tail (< kElems elements) of this tensor, handled by the tile that owns it
+    const long long tail0 = nunits * Op::kElems;
+    if (tail0 < n && tail0 >= e0 && tail0 < e0 + tile) {
+      if (threadIdx.x < n - tail0) Op::scalar(a, tail0 + threadIdx.x);
+    }
+  } else {
+    for (long long i = e0 + threadIdx.x; i < n && i < e0 + tile; i += kBlock) Op::scalar(a, i);
+  }
+}
+
+// Hex mantissa decode (FixedPointToFloatPointOp<string, T>, fixed_point.cc:255-257): one lane per
+// string; keeps the leading 64 bits of |m| and its bit length (mpf truncation composes to that).
+template <bool F64>
+__global__ __launch_bounds__(kBlock) void k_decode_hex(const char* chars, const long long* offs,
+                                                       const long long* E, void* y, long long n,
+                                                       int flag, long long* bad) {
+  const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  long long s = offs[i];
+  const long long end = offs[i + 1];
+  bool neg = false, ok = end > s;
+  if (ok && chars[s] == '-') {
+    neg = true;
+    ++s;
+    ok = end > s;
+  }
+  unsigned long long acc = 0;
+  int nbits = 0;
+  long long extra = 0;
+  for (long long j = s; j < end; ++j) {
+    const char c = chars[j];
+    int v;
+    if (c >= '0' && c <= '9') v = c - '0';
+    else if (c >= 'a' && c <= 'f') v = c - 'a' + 10;
+    else if (c >= 'A' && c <= 'F') v = c - 'A' + 10;
+    else { ok = false; break; }
+    if (nbits == 0) {
+      if (v) { acc = (unsigned long long)v; nbits = 64 - __clzll((long long)acc); }
+    } else if (nbits + 4 <= 64) {
+      acc = (acc << 4) | (unsigned long long)v;
+      nbits += 4;
+    } else {
+      const int room = 64 - nbits;
+      if (room > 0) { acc = (acc << room) | ((unsigned long long)v >> (4 - room)); nbits = 64; }
+      extra += 4 - room;
+    }
+  }
+  if (!ok) {
+    atomicMin((unsigned long long*)bad, (unsigned long long)i);
+    if (F64) ((unsigned long long*)y)[i] = 0x7FF8000000000000ull;
+    else ((unsigned*)y)[i] = 0x7FC00000u;
+    return;
+  }
+  const unsigned long long d = get_d_bits(acc, neg && acc != 0, E[i] + extra);
+  if (F64) ((unsigned long long*)y)[i] = d;
+  else ((float*)y)[i] = d2f(d, flag & EFL_FXP_FTZ);
+}
+
+// ------------------------------------------------------------------------------------------
+// launch configuration (tunable; see efl_fxp_tune)
+// ------------------------------------------------------------------------------------------
+
+std::atomic<int> g_enc_variant{0};   // 0 pair, 1 quad
+std::atomic<int> g_dec_variant{0};   // 0 pair, 1 quad
+std::atomic<int> g_tiles{4};         // K: units per lane per tile (1, 2, 4)
+std::atomic<int> g_grid_cap{0};      // 0: one tile per workgroup; else max workgroups
+std::atomic<int> g_nt{0};            // 0 none, 2 nt stores, 3 nt loads+stores
+
+template <class Op, int K, int NT>
+hipError_t launch_k(const typename Op::Args& a, long long nunits, hipStream_t s) {
+  const long long tile = (long long)kBlock * K;
+  long long grid = (nunits + tile - 1) / tile;
+  const int cap = g_grid_cap.load(std::memory_order_relaxed);
+  if (cap > 0 && grid > cap) grid = cap;
+  if (grid > 0x7FFFFFFFll) grid = 0x7FFFFFFFll;
+  if (grid == 0) return hipSuccess;
+  hipLaunchKernelGGL((k_stream<Op, K, NT>), dim3((unsigned)grid), dim3(kBlock), 0, s, a, nunits);
+  return hipGetLastError();
+}
+
+template <class Op, int K>
+hipError_t launch_nt(const typename Op::Args& a, long long nunits, hipStream_t s) {
+  switch (g_nt.load(std::memory_order_relaxed)) {
+    case 2: return launch_k<Op, K, 2>(a, nunits, s);
+    case 3: return launch_k<Op, K, 3>(a, nunits, s);
+    default: return launch_k<Op, K, 0>(a, nunits, s);
+  }
+}
+
+template <class Op>
+hipError_t launch_stream(const typename Op::Args& a, long long nunits, hipStream_t s) {
+  switch (g_tiles.load(std::memory_order_relaxed)) {
+    case 1: return launch_nt<Op, 1>(a, nunits, s);
+    case 2: return launch_nt<Op, 2>(a, nunits, s);
+    default: return launch_nt<Op, 4>(a, nunits, s);
+  }
+}
+
+template <class Op>
+hipError_t launch_scalar(const typename Op::Args& a, long long start, long long n, hipStream_t s) {
+  if (n <= start) return hipSuccess;
+  long long grid = (n - start + kBlock - 1) / kBlock;
+  if (grid > 4096) grid = 4096;
+  hipLaunchKernelGGL((k_scalar<Op>), dim3((unsigned)grid), dim3(kBlock), 0, s, a, start, n);
+  return hipGetLastError();
+}
+
+// vector path over the aligned prefix + scalar tail, or all-scalar when unaligned.
+template <class Op>
+hipError_t run(const typename Op::Args& a, const void* p0, const void* p1, const void* p2,
+               long long n, hipStream_t s) {
+  const uintptr_t need = 16;
+  if (aligned(p0, need) && aligned(p1, need) && aligned(p2, need)) {
+    const long long nunits = n / Op::kElems;
+    hipError_t e = launch_stream<Op>(a, nunits, s);
+    if (e != hipSuccess) return e;
+    return launch_scalar<Op>(a, nunits * Op::kElems, n, s);
+  }
+  return launch_scalar<Op>(a, 0, n, s);
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// error reporting
+// ------------------------------------------------------------------------------------------
+
+namespace {
+thread_local std::string t_err;
+}
+
+void set_error(const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  t_err = buf;
+}
+
+int hip_status(hipError_t e, const char* what) {
+  if (e == hipSuccess) return EFL_OK;
+  set_error("%s: %s", what, hipGetErrorString(e));
+  return EFL_E_INTERNAL;
+}
+
+}  // namespace efl
+
+using namespace efl;
+
+EFL_API const char* efl_version(void) { return "efl-hip 0.1.0 (gfx950)"; }
+
+EFL_API const char* efl_last_error(void) { return t_err.c_str(); }
+
+EFL_API int efl_fxp_tune(int kind, int value) {
+  std::atomic<int>* slot = nullptr;
+  switch (kind) {
+    case 0: if (value < 0 || value > 1) return EFL_E_INVALID_ARGUMENT; slot = &g_enc_variant; break;
+    case 1: if (value < 0 || value > 1) return EFL_E_INVALID_ARGUMENT; slot = &g_dec_variant; break;
+    case 2: if (value != 1 && value != 2 && value != 4) return EFL_E_INVALID_ARGUMENT; slot = &g_tiles; break;
+    case 3: if (value < 0) return EFL_E_INVALID_ARGUMENT; slot = &g_grid_cap; break;
+    case 4: if (value != 0 && value != 2 && value != 3) return EFL_E_INVALID_ARGUMENT; slot = &g_nt; break;
+    default: return EFL_E_INVALID_ARGUMENT;
+  }
+  return slot->exchange(value);
+}
+
+EFL_API int efl_fxp_encode(const void* x, int dtype, int64_t* mantissa, int64_t* exponent,
+                           int64_t n, int decrease_precision, void* stream) {
+  if (n < 0) { set_error("negative element count"); return EFL_E_INVALID_ARGUMENT; }
+  if (n == 0) return EFL_OK;
+  if (!x || !mantissa || !exponent) { set_error("null buffer"); return EFL_E_INVALID_ARGUMENT; }
+  hipStream_t s = (hipStream_t)stream;
+  EncArgs a{x, (long long*)mantissa, (long long*)exponent, decrease_precision ? 1 : 0};
+  hipError_t e;
+  switch (dtype) {
+    case EFL_DT_FLOAT:
+      e = g_enc_variant.load() == 1 ? run<EncF32Quad>(a, x, mantissa, exponent, n, s)
+                                    : run<EncF32Pair>(a, x, mantissa, exponent, n, s);
+      break;
+    case EFL_DT_DOUBLE: e = run<EncF64Pair>(a, x, mantissa, exponent, n, s); break;
+    case EFL_DT_INT8: e = run<EncIntPair<signed char, c2>>(a, x, mantissa, exponent, n, s); break;
+    case EFL_DT_INT16: e = run<EncIntPair<short, s2>>(a, x, mantissa, exponent, n, s); break;
+    case EFL_DT_INT32: e = run<EncIntPair<int, i2>>(a, x, mantissa, exponent, n, s); break;
+    case EFL_DT_INT64: e = run<EncIntPair<long long, ll2>>(a, x, mantissa, exponent, n, s); break;
+    default:
+      set_error("ConvertToFixedPoint: unsupported dtype %d (int8/16/32/64, float, double)", dtype);
+      return EFL_E_INVALID_ARGUMENT;
+  }
+  return hip_status(e, "efl_fxp_encode");
+}
+
+EFL_API int efl_fxp_decode(const int64_t* mantissa, const int64_t* exponent, void* y, int dtype,
+                           int64_t n_mantissa, int64_t n_exponent, int flags, void* stream) {
+  if (n_mantissa != n_exponent) {
+    set_error("mantissa and exponent should be the same size.");
+    return EFL_E_INVALID_ARGUMENT;
+  }
+  const int64_t n = n_mantissa;
+  if (n < 0) { set_error("negative element count"); return EFL_E_INVALID_ARGUMENT; }
+  if (n == 0) return EFL_OK;
+  if (!mantissa || !exponent || !y) { set_error("null buffer"); return EFL_E_INVALID_ARGUMENT; }
+  hipStream_t s = (hipStream_t)stream;
+  DecArgs a{(const long long*)mantissa, (const long long*)exponent, y, flags};
+  hipError_t e;
+  switch (dtype) {
+    case EFL_DT_FLOAT:
+      e = g_dec_variant.load() == 1 ? run<DecF32Quad>(a, mantissa, exponent, y, n, s)
+                                    : run<DecF32Pair>(a, mantissa, exponent, y, n, s);
+      break;
+    case EFL_DT_DOUBLE: e = run<DecF64Pair>(a, mantissa, exponent, y, n, s); break;
+    default:
+      set_error("FixedPointToFloatPoint: unsupported dtype %d (float, double)", dtype);
+      return EFL_E_INVALID_ARGUMENT;
+  }
+  return hip_status(e, "efl_fxp_decode");
+}
+
+EFL_API int efl_fxp_decode_hex(const char* chars, const int64_t* offsets, const int64_t* exponent,
+                               void* y, int dtype, int64_t n, int flags, int64_t* bad,
+                               void* stream) {
+  if (n < 0) { set_error("negative element count"); return EFL_E_INVALID_ARGUMENT; }
+  if (!bad) { set_error("null status word"); return EFL_E_INVALID_ARGUMENT; }
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = hipMemsetAsync(bad, 0xFF, sizeof(int64_t), s);   // -1 == no error
+  if (e != hipSuccess) return hip_status(e, "efl_fxp_decode_hex");
+  if (n == 0) return EFL_OK;
+  if (dtype != EFL_DT_FLOAT && dtype != EFL_DT_DOUBLE) {
+    set_error("FixedPointToFloatPoint: unsupported dtype %d (float, double)", dtype);
+    return EFL_E_INVALID_ARGUMENT;
+  }
+  const unsigned grid = (unsigned)((n + kBlock - 1) / kBlock);
+  if (dtype == EFL_DT_DOUBLE)
+    hipLaunchKernelGGL((k_decode_hex<true>), dim3(grid), dim3(kBlock), 0, s, chars,
+                       (const long long*)offsets, (const long long*)exponent, y, (long long)n,
+                       flags, (long long*)bad);
+  else
+    hipLaunchKernelGGL((k_decode_hex<false>), dim3(grid), dim3(kBlock), 0, s, chars,
+                       (const long long*)offsets, (const long long*)exponent, y, (long long)n,
+                       flags, (long long*)bad);
+  return hip_status(hipGetLastError(), "efl_fxp_decode_hex");
+}
+
+namespace {
+constexpr int kBatchK = 4;
+constexpr long long kMaxGridY = 65535;
+
+template <class Op>
+hipError_t launch_batched(const void* const* src, void* const* d0, void* const* d1,
+                          const long long* ns, long long count, long long max_n, int flag,
+                          hipStream_t s) {
+  const long long tile = (long long)kBlock * kBatchK * Op::kElems;
+  const long long gx = (max_n + tile - 1) / tile;
+  if (gx == 0 || count == 0) return hipSuccess;
+  for (long long b = 0; b < count; b += kMaxGridY) {
+    const long long gy = count - b < kMaxGridY ? count - b : kMaxGridY;
+    hipLaunchKernelGGL((k_batched<Op, kBatchK>), dim3((unsigned)gx, (unsigned)gy), dim3(kBlock), 0, s,
+                       src, d0, d1, ns, flag, b);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+}  // namespace
+
+EFL_API int efl_fxp_encode_batched(const void* const* xs, int dtype, int64_t* const* mantissas,
+                                   int64_t* const* exponents, const int64_t* ns, int64_t count,
+                                   int64_t max_n, int decrease_precision, void* stream) {
+  if (count < 0 || max_n < 0) { set_error("negative count"); return EFL_E_INVALID_ARGUMENT; }
+  if (count == 0 || max_n == 0) return EFL_OK;
+  hipStream_t s = (hipStream_t)stream;
+  auto d0 = (void* const*)mantissas;
+  auto d1 = (void* const*)exponents;
+  auto nn = (const long long*)ns;
+  const int f = decrease_precision ? 1 : 0;
+  hipError_t e;
+  switch (dtype) {
+    case EFL_DT_FLOAT: e = launch_batched<EncF32Pair>(xs, d0, d1, nn, count, max_n, f, s); break;
+    case EFL_DT_DOUBLE: e = launch_batched<EncF64Pair>(xs, d0, d1, nn, count, max_n, f, s); break;
+    case EFL_DT_INT8: e = launch_batched<EncIntPair<signed char, c2>>(xs, d0, d1, nn, count, max_n, f, s); break;
+    case EFL_DT_INT16: e = launch_batched<EncIntPair<short, s2>>(xs, d0, d1, nn, count, max_n, f, s); break;
+    case EFL_DT_INT32: e = launch_batched<EncIntPair<int, i2>>(xs, d0, d1, nn, count, max_n, f, s); break;
+    case EFL_DT_INT64: e = launch_batched<EncIntPair<long long, ll2>>(xs, d0, d1, nn, count, max_n, f, s); break;
+    default:
+      set_error("ConvertToFixedPoint: unsupported dtype %d", dtype);
+      return EFL_E_INVALID_ARGUMENT;
+  }
+  return hip_status(e, "efl_fxp_encode_batched");
+}
+
+EFL_API int efl_fxp_decode_batched(const int64_t* const* mantissas, const int64_t* const* exponents,
+                                   void* const* ys, int dtype, const int64_t* ns, int64_t count,
+                                   int64_t max_n, int flags, void* stream) {
+  if (count < 0 || max_n < 0) { set_error("negative count"); return EFL_E_INVALID_ARGUMENT; }
+  if (count == 0 || max_n == 0) return EFL_OK;
+  hipStream_t s = (hipStream_t)stream;
+  auto src = (const void* const*)mantissas;
+  auto d0 = (void* const*)exponents;
+  auto nn = (const long long*)ns;
+  hipError_t e;
+  switch (dtype) {
+    case EFL_DT_FLOAT: e = launch_batched<DecF32Pair>(src, d0, ys, nn, count, max_n, flags, s); break;
+    case EFL_DT_DOUBLE: e = launch_batched<DecF64Pair>(src, d0, ys, nn, count, max_n, flags, s); break;
+    default:
+      set_error("FixedPointToFloatPoint: unsupported dtype %d", dtype);
+      return EFL_E_INVALID_ARGUMENT;
+  }
+  return hip_status(e, "efl_fxp_decode_batched");
+}

@@ -1,0 +1,18 @@
+"""efl — MI355X-native drop-in for the forward-encryption path of EFLS-train.
+
+Public names mirror efls-train/python/efl (exporter registry, efl/__init__.py:47):
+  efl.paillier.fixedpoint.{encode, decode, Tensor}
+  efl.HexTensor (the DT_STRING stand-in), efl.lib.ops (the `fed_ops` namespace)
+The kernels live in libefl_hip.so (C ABI: include/efl_hip.h); there is no CPU fallback.
+"""
+from efl import exporter
+from efl import errors
+from efl import lib
+from efl.lib import set_flush_denormal, flush_denormal
+from efl.privacy import encryptor_utils
+from efl.privacy import paillier
+from efl.privacy.hex_tensor import HexTensor
+
+exporter.filldict(globals())
+
+__version__ = "0.1.0"

@@ -1,0 +1,302 @@
+"""Loads libefl_hip.so (the MI355X kernels behind the C ABI in include/efl_hip.h) and exposes
+the op functions under the names the reference's `fed_ops` has.
+
+Reference: efls-train/python/efl/lib.py:24-28 loads libefl.so with `tf.load_op_library` and the
+callers use `fed_ops.convert_to_fixed_point`, `fed_ops.fixed_point_to_float_point`, ...
+(efls-train/python/efl/privacy/paillier.py:56-155). Here `efl.lib.ops` is that namespace, over
+torch tensors instead of TF graph tensors.
+
+There is no CPU fallback: the library must be present (ImportError otherwise) and every op needs a
+ROCm device (a CPU input is staged through the GPU and the result copied back).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import types
+
+import numpy as np
+import torch
+
+from efl import errors
+
+_LIB_DIR = os.path.dirname(os.path.realpath(__file__))
+LIB_PATH = os.path.join(_LIB_DIR, "libefl_hip.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"{LIB_PATH} is missing: build it with `make -C elastic-federated-learning-solution_amd` "
+        "(or __graft_entry__.build()). The efl ops have no CPU fallback.")
+
+_lib = ctypes.CDLL(LIB_PATH)
+
+_vp, _i64, _i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+_SIGS = {
+    "efl_version": ([], ctypes.c_char_p),
+    "efl_last_error": ([], ctypes.c_char_p),
+    "efl_fxp_tune": ([_i32, _i32], _i32),
+    "efl_fxp_encode": ([_vp, _i32, _vp, _vp, _i64, _i32, _vp], _i32),
+    "efl_fxp_decode": ([_vp, _vp, _vp, _i32, _i64, _i64, _i32, _vp], _i32),
+    "efl_fxp_decode_hex": ([_vp, _vp, _vp, _vp, _i32, _i64, _i32, _vp, _vp], _i32),
+    "efl_fxp_encode_batched": ([_vp, _i32, _vp, _vp, _vp, _i64, _i64, _i32, _vp], _i32),
+    "efl_fxp_decode_batched": ([_vp, _vp, _vp, _i32, _vp, _i64, _i64, _i32, _vp], _i32),
+}
+for _name, (_args, _ret) in _SIGS.items():
+    _f = getattr(_lib, _name)
+    _f.argtypes = _args
+    _f.restype = _ret
+
+# TensorFlow DataType numbers (types.proto), as used by the C ABI and the wire format.
+DT_FLOAT, DT_DOUBLE, DT_INT32, DT_INT16, DT_INT8, DT_STRING, DT_INT64 = 1, 2, 3, 5, 6, 7, 9
+_TORCH_TO_DT = {torch.float32: DT_FLOAT, torch.float64: DT_DOUBLE, torch.int32: DT_INT32,
+                torch.int16: DT_INT16, torch.int8: DT_INT8, torch.int64: DT_INT64}
+_DT_TO_TORCH = {v: k for k, v in _TORCH_TO_DT.items()}
+
+_flush_denormal = False
+
+
+def raw():
+    """The ctypes handle of libefl_hip.so."""
+    return _lib
+
+
+def version() -> str:
+    return _lib.efl_version().decode()
+
+
+def set_flush_denormal(enabled: bool) -> bool:
+    """Decode float32 results below the normal range to signed zero, as the reference does inside
+    TensorFlow's threadpool threads (MXCSR FTZ|DAZ). Default False = the bare reference loop
+    (SURVEY.md Appendix A). Returns the previous setting."""
+    global _flush_denormal
+    old, _flush_denormal = _flush_denormal, bool(enabled)
+    return old
+
+
+def flush_denormal() -> bool:
+    return _flush_denormal
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        raise errors.from_code(-rc, _lib.efl_last_error().decode())
+
+
+def to_torch_dtype(dtype) -> torch.dtype:
+    """Accepts torch dtypes, numpy dtypes, TF-style names ('float32') and DataType numbers."""
+    if isinstance(dtype, torch.dtype):
+        return dtype
+    if isinstance(dtype, int) and dtype in _DT_TO_TORCH:
+        return _DT_TO_TORCH[dtype]
+    name = getattr(dtype, "name", None) or str(dtype)
+    name = name.replace("tf.", "").replace("torch.", "")
+    table = {"float32": torch.float32, "float": torch.float32, "float64": torch.float64,
+             "double": torch.float64, "int8": torch.int8, "int16": torch.int16,
+             "int32": torch.int32, "int64": torch.int64}
+    if name in table:
+        return table[name]
+    try:
+        return to_torch_dtype(np.dtype(dtype).name)
+    except TypeError:
+        pass
+    raise errors.InvalidArgumentError(f"unsupported dtype {dtype!r}")
+
+
+def dt_code(dtype: torch.dtype) -> int:
+    try:
+        return _TORCH_TO_DT[dtype]
+    except KeyError:
+        raise errors.InvalidArgumentError(f"unsupported dtype {dtype}") from None
+
+
+_device_checked = False
+
+
+def require_gpu() -> torch.device:
+    """The ROCm device the ops run on; raises if there is none (no CPU fallback)."""
+    global _device_checked
+    if not torch.cuda.is_available():
+        raise RuntimeError("efl: no ROCm GPU visible; the forward-encryption ops run only on "
+                           "MI355X (gfx950) through libefl_hip.so")
+    if not _device_checked:
+        arch = torch.cuda.get_device_properties(0).gcnArchName
+        if not arch.startswith("gfx950"):
+            raise RuntimeError(f"efl: libefl_hip.so is built for gfx950, device is {arch}")
+        _device_checked = True
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def stream_handle(device: torch.device | None = None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def as_tensor(x) -> torch.Tensor:
+    if isinstance(x, torch.Tensor):
+        return x
+    return torch.as_tensor(np.asarray(x))
+
+
+def on_device(t: torch.Tensor):
+    """Contiguous device view of `t` (staging host tensors through H2D), plus the device the
+    result should be returned on."""
+    home = t.device
+    if t.is_cuda:
+        return t.contiguous(), home
+    dev = require_gpu()
+    return t.contiguous().to(dev, non_blocking=t.is_pinned()), home
+
+
+def back(t: torch.Tensor, home: torch.device) -> torch.Tensor:
+    if t.device == home:
+        return t
+    return t.to(home)
+
+
+# ----------------------------------------------------------------------------------------------
+# ops (fed_ops names)
+# ----------------------------------------------------------------------------------------------
+
+def convert_to_fixed_point(t, decrease_precision=None):
+    """REGISTER_OP("ConvertToFixedPoint") (efls-train/cc/efl/math/fixed_point.cc:24-40).
+    Returns (mantissa int64, exponent int64) of t's shape, on t's device."""
+    t = as_tensor(t)
+    code = dt_code(t.dtype)
+    x, home = on_device(t)
+    M = torch.empty(x.shape, dtype=torch.int64, device=x.device)
+    E = torch.empty(x.shape, dtype=torch.int64, device=x.device)
+    check(_lib.efl_fxp_encode(x.data_ptr(), code, M.data_ptr(), E.data_ptr(), x.numel(),
+                              int(bool(decrease_precision)), stream_handle(x.device)))
+    return back(M, home), back(E, home)
+
+
+def _hex_list(m):
+    """Flatten a string-tensor stand-in (numpy object/bytes array, nested list) to list[bytes]."""
+    if isinstance(m, (bytes, str)):
+        m = [m]
+    arr = np.asarray(m, dtype=object).reshape(-1)
+    return [s.encode() if isinstance(s, str) else bytes(s) for s in arr], np.shape(m)
+
+
+def fixed_point_to_float_point(mantissa, exponent, dtype=torch.float32, flush_denormal=None):
+    """REGISTER_OP("FixedPointToFloatPoint") (fixed_point.cc:201-214): y = mantissa * 2^exponent.
+    `mantissa` is an int64 tensor, or (the reference's DT_STRING form) hex strings: a
+    `efl.HexTensor`, numpy array / list of str|bytes. Output on exponent's device."""
+    dtype = to_torch_dtype(dtype)
+    if dtype not in (torch.float32, torch.float64):
+        raise errors.InvalidArgumentError(f"FixedPointToFloatPoint: dtype must be float or double, got {dtype}")
+    ftz = _flush_denormal if flush_denormal is None else bool(flush_denormal)
+    flags = 1 if ftz else 0
+    exponent = as_tensor(exponent)
+    from efl.privacy.hex_tensor import HexTensor  # local import: avoids a cycle at import time
+    if isinstance(mantissa, HexTensor) or not isinstance(mantissa, torch.Tensor) and \
+            np.asarray(mantissa, dtype=object).dtype == object and _looks_textual(mantissa):
+        hx = mantissa if isinstance(mantissa, HexTensor) else HexTensor.from_strings(mantissa)
+        return _decode_hex(hx, exponent, dtype, flags)
+    mantissa = as_tensor(mantissa)
+    if mantissa.dtype != torch.int64 or exponent.dtype != torch.int64:
+        raise errors.InvalidArgumentError("FixedPointToFloatPoint: mantissa and exponent must be int64")
+    m, home = on_device(mantissa)
+    e, _ = on_device(exponent)
+    if e.device != m.device:
+        e = e.to(m.device)
+    y = torch.empty(m.shape, dtype=dtype, device=m.device)
+    check(_lib.efl_fxp_decode(m.data_ptr(), e.data_ptr(), y.data_ptr(), dt_code(dtype), m.numel(),
+                              e.numel(), flags, stream_handle(m.device)))
+    return back(y, home)
+
+
+def _looks_textual(m) -> bool:
+    a = np.asarray(m, dtype=object).reshape(-1)
+    return a.size == 0 or isinstance(a[0], (str, bytes, bytearray))
+
+
+def _decode_hex(hx, exponent, dtype, flags):
+    if hx.numel() != exponent.numel():
+        raise errors.InvalidArgumentError("mantissa and exponent should be the same size.")
+    e, home = on_device(exponent)
+    dev = e.device
+    chars, offs = hx.device_buffers(dev)
+    y = torch.empty(tuple(exponent.shape), dtype=dtype, device=dev)
+    bad = torch.empty(1, dtype=torch.int64, device=dev)
+    check(_lib.efl_fxp_decode_hex(chars.data_ptr(), offs.data_ptr(), e.data_ptr(), y.data_ptr(),
+                                  dt_code(dtype), hx.numel(), flags, bad.data_ptr(),
+                                  stream_handle(dev)))
+    b = int(bad.item())
+    if b >= 0:
+        raise errors.InvalidArgumentError(
+            f"FixedPointToFloatPoint: mantissa[{b}] = {hx.strings()[b]!r} is not a hex integer")
+    return back(y, home)
+
+
+def _ptr_table(ts, dev):
+    return torch.tensor([t.data_ptr() for t in ts], dtype=torch.int64).to(dev)
+
+
+def convert_to_fixed_point_batched(tensors, decrease_precision=None):
+    """One launch for a list of device tensors of one dtype (BASELINE config 3, sparse-rec
+    embedding slices). Returns ([mantissa], [exponent])."""
+    if not tensors:
+        return [], []
+    dev = tensors[0].device
+    if not dev.type == "cuda":
+        raise errors.InvalidArgumentError("batched ops take device tensors")
+    code = dt_code(tensors[0].dtype)
+    xs = [t.contiguous() for t in tensors]
+    if any(t.dtype != xs[0].dtype or t.device != dev for t in xs):
+        raise errors.InvalidArgumentError("batched encode: tensors must share dtype and device")
+    Ms = [torch.empty(t.shape, dtype=torch.int64, device=dev) for t in xs]
+    Es = [torch.empty(t.shape, dtype=torch.int64, device=dev) for t in xs]
+    tables = BatchTables(xs, Ms, Es)
+    check(_lib.efl_fxp_encode_batched(*tables.args(), code, int(bool(decrease_precision)),
+                                      stream_handle(dev)))
+    return Ms, Es
+
+
+class BatchTables:
+    """Device pointer/length tables for the batched ABI (built once, reusable across launches)."""
+
+    def __init__(self, srcs, d0s, d1s):
+        dev = srcs[0].device
+        self.keep = (srcs, d0s, d1s)
+        self.src = _ptr_table(srcs, dev)
+        self.d0 = _ptr_table(d0s, dev)
+        self.d1 = _ptr_table(d1s, dev)
+        self.ns = torch.tensor([t.numel() for t in srcs], dtype=torch.int64).to(dev)
+        self.count = len(srcs)
+        self.max_n = max(t.numel() for t in srcs)
+
+    def args(self):
+        return self.src.data_ptr(), self.d0.data_ptr(), self.d1.data_ptr(), self.ns.data_ptr(), \
+            self.count, self.max_n
+
+
+def encode_batched_into(tables: BatchTables, dtype_code: int, decrease_precision=False, stream=None):
+    src, d0, d1, ns, count, max_n = tables.args()
+    check(_lib.efl_fxp_encode_batched(src, dtype_code, d0, d1, ns, count, max_n,
+                                      int(bool(decrease_precision)),
+                                      stream if stream is not None else stream_handle()))
+
+
+def decode_batched_into(tables: BatchTables, dtype_code: int, flags=0, stream=None):
+    src, d0, d1, ns, count, max_n = tables.args()
+    check(_lib.efl_fxp_decode_batched(src, d0, d1, dtype_code, ns, count, max_n, flags,
+                                      stream if stream is not None else stream_handle()))
+
+
+def fixed_point_to_float_point_batched(mantissas, exponents, dtype=torch.float32):
+    if not mantissas:
+        return []
+    dtype = to_torch_dtype(dtype)
+    dev = mantissas[0].device
+    ys = [torch.empty(m.shape, dtype=dtype, device=dev) for m in mantissas]
+    tables = BatchTables(mantissas, exponents, ys)
+    decode_batched_into(tables, dt_code(dtype), 1 if _flush_denormal else 0, stream_handle(dev))
+    return ys
+
+
+ops = types.SimpleNamespace(
+    convert_to_fixed_point=convert_to_fixed_point,
+    fixed_point_to_float_point=fixed_point_to_float_point,
+    convert_to_fixed_point_batched=convert_to_fixed_point_batched,
+    fixed_point_to_float_point_batched=fixed_point_to_float_point_batched,
+)

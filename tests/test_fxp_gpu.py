@@ -1,0 +1,259 @@
+"""GPU parity: libefl_hip.so's Stage-F kernels vs the oracle and the golden fixtures.
+
+Bar: bit-exact (integer work on IEEE bit patterns; the decode reproduces GMP's truncating
+mpf_get_d). All calls go through the C ABI via the `efl` package.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import fxp
+
+pytestmark = pytest.mark.gpu
+
+G = np.load(os.path.join(GOLDEN, "fxp_golden.npz"))
+H = np.load(os.path.join(GOLDEN, "fxp_hex_golden.npz"))
+
+
+@pytest.fixture(scope="module")
+def efl():
+    import efl as _efl
+    _efl.lib.require_gpu()
+    return _efl
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def host(t):
+    return t.cpu().numpy()
+
+
+def bits32(t):
+    return host(t).view(np.uint32)
+
+
+def bits64(t):
+    return host(t).view(np.uint64)
+
+
+# ------------------------------------------------------------------------------ golden sets
+
+@pytest.mark.parametrize("dp", [0, 1])
+def test_encode_f32_golden(efl, dp):
+    x = dev(G["f32_bits"].view(np.float32))
+    fp = efl.paillier.fixedpoint.encode(x, decrease_precision=bool(dp))
+    assert np.array_equal(host(fp.mantissa), G[f"f32_M_dp{dp}"])
+    assert np.array_equal(host(fp.exponent), G[f"f32_E_dp{dp}"])
+
+
+@pytest.mark.parametrize("dp", [0, 1])
+@pytest.mark.parametrize("ftz", [0, 1])
+def test_round_trip_f32_golden(efl, dp, ftz):
+    M, E = dev(G[f"f32_M_dp{dp}"]), dev(G[f"f32_E_dp{dp}"])
+    y = efl.lib.ops.fixed_point_to_float_point(M, E, torch.float32, flush_denormal=bool(ftz))
+    assert np.array_equal(bits32(y), G[f"f32_rt_dp{dp}_ftz{ftz}"])
+
+
+@pytest.mark.parametrize("dp", [0, 1])
+def test_f64_golden(efl, dp):
+    x = dev(G["f64_bits"].view(np.float64))
+    fp = efl.paillier.fixedpoint.encode(x, decrease_precision=bool(dp))
+    assert np.array_equal(host(fp.mantissa), G[f"f64_M_dp{dp}"])
+    assert np.array_equal(host(fp.exponent), G[f"f64_E_dp{dp}"])
+    y = efl.paillier.fixedpoint.decode(fp, dtype=torch.float64)
+    assert np.array_equal(bits64(y), G[f"f64_rt_dp{dp}"])
+
+
+@pytest.mark.parametrize("name", ["int8", "int16", "int32", "int64"])
+def test_encode_int_golden(efl, name):
+    fp = efl.paillier.fixedpoint.encode(dev(G[name]))
+    assert np.array_equal(host(fp.mantissa), G[name].astype(np.int64))
+    assert not host(fp.exponent).any()
+
+
+@pytest.mark.parametrize("ftz", [0, 1])
+def test_decode_i64_golden(efl, ftz):
+    y = efl.lib.ops.fixed_point_to_float_point(dev(G["dec_M"]), dev(G["dec_E"]), "float32",
+                                               flush_denormal=bool(ftz))
+    assert np.array_equal(bits32(y), G[f"dec_f32_ftz{ftz}"])
+
+
+def test_decode_i64_f64_golden(efl):
+    y = efl.lib.ops.fixed_point_to_float_point(dev(G["dec_M"]), dev(G["dec_E"]), torch.float64)
+    assert np.array_equal(bits64(y), G["dec_f64"])
+
+
+def _hex():
+    b, o = H["buf"].tobytes(), H["offs"]
+    return [b[o[i]:o[i + 1]] for i in range(o.size - 1)]
+
+
+@pytest.mark.parametrize("ftz", [0, 1])
+def test_decode_hex_golden(efl, ftz):
+    hx = efl.HexTensor.from_strings(np.array(_hex(), dtype=object))
+    y = efl.lib.ops.fixed_point_to_float_point(hx, dev(H["E"]), torch.float32, flush_denormal=bool(ftz))
+    assert np.array_equal(bits32(y), H[f"f32_ftz{ftz}"])
+    y64 = efl.lib.ops.fixed_point_to_float_point(hx, dev(H["E"]), torch.float64)
+    assert np.array_equal(bits64(y64), H["f64"])
+
+
+def test_decode_hex_malformed(efl):
+    hx = efl.HexTensor.from_strings(["1f", "xyz", "-3"])
+    with pytest.raises(efl.errors.InvalidArgumentError, match=r"mantissa\[1\]"):
+        efl.lib.ops.fixed_point_to_float_point(hx, dev(np.zeros(3, np.int64)))
+
+
+# ---------------------------------------------------------------- seeded inputs vs oracle
+
+SIZES = [0, 1, 2, 3, 5, 127, 255, 256, 1023, 4097, 65537, (1 << 20) + 3]
+
+
+def rand_bits(n, seed):
+    rng = np.random.default_rng(seed)
+    x = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    x[: n // 3] = rng.standard_normal(n // 3).astype(np.float32).view(np.uint32)
+    return x
+
+
+@pytest.mark.parametrize("n", SIZES)
+@pytest.mark.parametrize("dp", [0, 1])
+def test_f32_vs_oracle(efl, n, dp):
+    xb = rand_bits(n, n + 17 * dp)
+    x = xb.view(np.float32)
+    fp = efl.paillier.fixedpoint.encode(dev(x), decrease_precision=bool(dp))
+    Mo, Eo = fxp.encode(x, dp)
+    assert np.array_equal(host(fp.mantissa), Mo) and np.array_equal(host(fp.exponent), Eo)
+    y = efl.paillier.fixedpoint.decode(fp)
+    assert np.array_equal(bits32(y), fxp.decode(Mo, Eo).view(np.uint32))
+
+
+@pytest.mark.parametrize("n", [1, 3, 1000, 4099])
+def test_f64_and_int_vs_oracle(efl, n):
+    rng = np.random.default_rng(n)
+    xd = rng.integers(0, 1 << 63, n, dtype=np.uint64).view(np.float64) * np.where(rng.random(n) < .5, -1, 1)
+    fp = efl.paillier.fixedpoint.encode(dev(xd))
+    Mo, Eo = fxp.encode(xd)
+    assert np.array_equal(host(fp.mantissa), Mo) and np.array_equal(host(fp.exponent), Eo)
+    assert np.array_equal(bits64(efl.paillier.fixedpoint.decode(fp, torch.float64)),
+                          fxp.decode(Mo, Eo, np.float64).view(np.uint64))
+    for dt in (np.int8, np.int16, np.int32, np.int64):
+        xi = rng.integers(np.iinfo(dt).min, np.iinfo(dt).max, n, dtype=np.int64).astype(dt)
+        fp = efl.paillier.fixedpoint.encode(dev(xi))
+        assert np.array_equal(host(fp.mantissa), xi.astype(np.int64))
+
+
+@pytest.mark.parametrize("offset", [1, 2, 3])
+def test_unaligned_views(efl, offset):
+    n = 10007
+    x = rand_bits(n + offset, 99).view(np.float32)
+    xt = dev(x)[offset:]
+    assert xt.data_ptr() % 16 != 0
+    fp = efl.paillier.fixedpoint.encode(xt)
+    Mo, Eo = fxp.encode(x[offset:])
+    assert np.array_equal(host(fp.mantissa), Mo)
+    Mt = torch.empty(n + offset, dtype=torch.int64, device="cuda")[offset:]
+    Et = torch.empty(n + offset, dtype=torch.int64, device="cuda")[offset:]
+    Mt.copy_(fp.mantissa)
+    Et.copy_(fp.exponent)
+    y = efl.lib.ops.fixed_point_to_float_point(Mt, Et)
+    assert np.array_equal(bits32(y), fxp.decode(Mo, Eo).view(np.uint32))
+
+
+def test_shapes_and_host_staging(efl):
+    x = torch.randn(7, 33, 5, generator=torch.Generator().manual_seed(3))
+    fp = efl.paillier.fixedpoint.encode(x)          # CPU tensor in -> CPU tensors out
+    assert fp.mantissa.device.type == "cpu" and fp.mantissa.shape == x.shape
+    Mo, Eo = fxp.encode(x.numpy())
+    assert np.array_equal(fp.mantissa.numpy(), Mo) and np.array_equal(fp.exponent.numpy(), Eo)
+    y = efl.paillier.fixedpoint.decode(fp)
+    assert y.device.type == "cpu" and torch.equal(y, x)
+
+
+def test_errors(efl):
+    with pytest.raises(efl.errors.InvalidArgumentError, match="same size"):
+        efl.lib.ops.fixed_point_to_float_point(dev(np.zeros(4, np.int64)), dev(np.zeros(5, np.int64)))
+    with pytest.raises(efl.errors.InvalidArgumentError):
+        efl.paillier.fixedpoint.encode(torch.zeros(4, dtype=torch.uint8, device="cuda"))
+    with pytest.raises(efl.errors.InvalidArgumentError):
+        efl.lib.ops.fixed_point_to_float_point(dev(np.zeros(4, np.int64)), dev(np.zeros(4, np.int64)),
+                                               torch.int32)
+
+
+@pytest.mark.parametrize("knob", [(0, 1), (1, 1), (2, 1), (2, 2), (3, 512), (4, 2), (4, 3)])
+def test_tuning_variants_identical(efl, knob):
+    lib = efl.lib.raw()
+    n = (1 << 18) + 7
+    x = rand_bits(n, 7).view(np.float32)
+    Mo, Eo = fxp.encode(x)
+    yo = fxp.decode(Mo, Eo).view(np.uint32)
+    prev = lib.efl_fxp_tune(*knob)
+    try:
+        fp = efl.paillier.fixedpoint.encode(dev(x))
+        assert np.array_equal(host(fp.mantissa), Mo) and np.array_equal(host(fp.exponent), Eo)
+        assert np.array_equal(bits32(efl.paillier.fixedpoint.decode(fp)), yo)
+    finally:
+        lib.efl_fxp_tune(knob[0], prev)
+
+
+# ----------------------------------------------------------------------------- batched
+
+def test_batched_ragged(efl):
+    rng = np.random.default_rng(11)
+    sizes = [0, 1, 2, 3, 16384, 4097, 100000] + [int(s) for s in rng.integers(1, 40000, 200)]
+    xs_np = [rand_bits(s, i).view(np.float32) for i, s in enumerate(sizes)]
+    xs = [dev(a) for a in xs_np]
+    xs[5] = dev(np.concatenate([[0], xs_np[5]]).astype(np.float32))[1:]   # unaligned member
+    Ms, Es = efl.lib.ops.convert_to_fixed_point_batched(xs, decrease_precision=False)
+    for a, M, E in zip(xs_np, Ms, Es):
+        Mo, Eo = fxp.encode(a)
+        assert np.array_equal(host(M), Mo) and np.array_equal(host(E), Eo)
+    ys = efl.lib.ops.fixed_point_to_float_point_batched(Ms, Es)
+    for a, y in zip(xs_np, ys):
+        Mo, Eo = fxp.encode(a)
+        assert np.array_equal(bits32(y), fxp.decode(Mo, Eo).view(np.uint32))
+
+
+def test_batched_embedding_slices(efl):
+    """BASELINE config 3 shape: 4096 x 64 KiB fp32 slices, N(0, 0.01), seed 1."""
+    g = torch.Generator(device="cuda").manual_seed(1)
+    big = torch.randn(4096 * 16384, device="cuda", generator=g) * 0.01
+    xs = list(big.view(4096, 16384).unbind(0))
+    Ms, Es = efl.lib.ops.convert_to_fixed_point_batched(xs)
+    ys = efl.lib.ops.fixed_point_to_float_point_batched(Ms, Es)
+    y = torch.stack(ys)
+    assert torch.equal(y.view(-1)[big != 0], big[big != 0])
+    idx = np.random.default_rng(0).integers(0, 4096, 8)
+    for i in idx:
+        Mo, Eo = fxp.encode(host(xs[i]))
+        assert np.array_equal(host(Ms[i]), Mo) and np.array_equal(host(Es[i]), Eo)
+
+
+# ------------------------------------------------------------------- full size (256 MiB)
+
+def test_full_size_properties(efl):
+    """BASELINE config 2 size (67,108,864 fp32): size-independent properties + sampled bits."""
+    n = 1 << 26
+    g = torch.Generator(device="cuda").manual_seed(0)
+    x = torch.randn(n, device="cuda", generator=g)
+    fp = efl.paillier.fixedpoint.encode(x)
+    y = efl.paillier.fixedpoint.decode(fp)
+    nz = x != 0
+    # round trip is the identity on every non-zero N(0,1) value; zeros become 2^-127
+    assert torch.equal(y[nz], x[nz])
+    assert torch.all(y[~nz].view(torch.int32) == 0x00400000)
+    # mantissas are odd (normalised) except the zero quirk, |M| < 2^24
+    M, E = fp.mantissa, fp.exponent
+    assert torch.all((M[nz] & 1) == 1) and torch.all(M.abs() < (1 << 24))
+    # 1 % sampled bit compare against the oracle
+    idx = torch.from_numpy(np.random.default_rng(0).integers(0, n, n // 100)).cuda()
+    xs = host(x[idx])
+    Mo, Eo = fxp.encode(xs)
+    assert np.array_equal(host(M[idx]), Mo) and np.array_equal(host(E[idx]), Eo)
+    # checksum of the whole output against an oracle pass over the whole tensor
+    Mo_all, Eo_all = fxp.encode(host(x))
+    assert int(M.sum()) == int(Mo_all.sum()) and int(E.sum()) == int(Eo_all.sum())

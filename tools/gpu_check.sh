@@ -1,0 +1,31 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, bench, variant sweep, rocprofv3 kernel-trace + PMC passes.
+# Every GPU step has its own time limit; steps are chained with && so the first failure ends it.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+O=gpurun_out
+mkdir -p $O
+STAGE=${1:-all}
+run_tests() { timeout -k 10 900 python -m pytest tests -m gpu -x -q > $O/pytest_gpu.log 2>&1; }
+run_smoke() { timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1; }
+run_bench() { timeout -k 10 300 python bench.py --steps 50 --warmup 5 > $O/bench.json 2> $O/bench.err; }
+run_sweep() { timeout -k 10 300 python tools/sweep_fxp.py > $O/sweep.jsonl 2> $O/sweep.err; }
+run_prof() {
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_trace -o run --output-format csv \
+      -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > $O/prof_trace.log 2>&1 &&
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/prof_fetch -o run --output-format csv \
+      -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > $O/prof_fetch.log 2>&1 &&
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/prof_write -o run --output-format csv \
+      -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > $O/prof_write.log 2>&1
+}
+case $STAGE in
+  all) run_tests && run_smoke && run_bench && run_sweep && run_prof ;;
+  tests) run_tests ;;
+  bench) run_bench && run_sweep ;;
+  prof) run_prof ;;
+  *) echo "unknown stage $STAGE"; exit 2 ;;
+esac
+rc=$?
+echo "gpu_check $STAGE rc=$rc"
+exit $rc
