@@ -247,8 +247,7 @@ def convert_to_fixed_point_batched(tensors, decrease_precision=None):
     Ms = [torch.empty(t.shape, dtype=torch.int64, device=dev) for t in xs]
     Es = [torch.empty(t.shape, dtype=torch.int64, device=dev) for t in xs]
     tables = BatchTables(xs, Ms, Es)
-    check(_lib.efl_fxp_encode_batched(*tables.args(), code, int(bool(decrease_precision)),
-                                      stream_handle(dev)))
+    encode_batched_into(tables, code, decrease_precision, stream_handle(dev))
     return Ms, Es
 
 

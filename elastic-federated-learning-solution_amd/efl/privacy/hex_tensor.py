@@ -95,7 +95,8 @@ class HexTensor:
     def device_buffers(self, device):
         """(chars uint8, offsets int64) on `device`, cached."""
         if self._dev_cache is None or self._dev_cache[0] != device:
-            chars = torch.from_numpy(self.buf if self.buf.size else np.zeros(1, np.uint8)).to(device)
+            host = self.buf if self.buf.size else np.zeros(1, np.uint8)
+            chars = torch.from_numpy(np.array(host, copy=not host.flags.writeable)).to(device)
             offs = torch.from_numpy(self.offs).to(device)
             self._dev_cache = (device, chars, offs)
         return self._dev_cache[1], self._dev_cache[2]

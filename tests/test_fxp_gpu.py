@@ -135,7 +135,8 @@ def test_f32_vs_oracle(efl, n, dp):
 @pytest.mark.parametrize("n", [1, 3, 1000, 4099])
 def test_f64_and_int_vs_oracle(efl, n):
     rng = np.random.default_rng(n)
-    xd = rng.integers(0, 1 << 63, n, dtype=np.uint64).view(np.float64) * np.where(rng.random(n) < .5, -1, 1)
+    xb = rng.integers(0, 1 << 63, n, dtype=np.uint64) | (rng.integers(0, 2, n, dtype=np.uint64) << np.uint64(63))
+    xd = xb.view(np.float64)
     fp = efl.paillier.fixedpoint.encode(dev(xd))
     Mo, Eo = fxp.encode(xd)
     assert np.array_equal(host(fp.mantissa), Mo) and np.array_equal(host(fp.exponent), Eo)
@@ -207,7 +208,7 @@ def test_batched_ragged(efl):
     sizes = [0, 1, 2, 3, 16384, 4097, 100000] + [int(s) for s in rng.integers(1, 40000, 200)]
     xs_np = [rand_bits(s, i).view(np.float32) for i, s in enumerate(sizes)]
     xs = [dev(a) for a in xs_np]
-    xs[5] = dev(np.concatenate([[0], xs_np[5]]).astype(np.float32))[1:]   # unaligned member
+    xs[5] = dev(np.concatenate([[0], xs_np[5].view(np.uint32)]).astype(np.uint32).view(np.float32))[1:]
     Ms, Es = efl.lib.ops.convert_to_fixed_point_batched(xs, decrease_precision=False)
     for a, M, E in zip(xs_np, Ms, Es):
         Mo, Eo = fxp.encode(a)
