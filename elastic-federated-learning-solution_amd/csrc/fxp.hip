@@ -259,29 +259,29 @@ struct DecF64Pair {
 // kernels
 // ------------------------------------------------------------------------------------------
 
-// Streaming kernel: tiles of kBlock*K units; a workgroup walks tiles blockIdx.x, +gridDim.x, ...
-// Inside a full tile every lane issues its K loads back to back before any store (K 16-B loads
-// in flight per lane), then transforms and stores. Tile t of a wave touches one contiguous span.
-template <class Op, int K, int NT>
-__global__ __launch_bounds__(kBlock) void k_stream(typename Op::Args a, long long nunits) {
-  const long long tile = (long long)kBlock * K;
+// Streaming kernel: tiles of B*K units; a workgroup walks tiles blockIdx.x, +gridDim.x, ...
+// Inside a full tile every lane issues its K loads back to back before any store, then transforms
+// and stores. Tile t of a wave touches one contiguous span.
+template <class Op, int B, int K, int NT>
+__global__ __launch_bounds__(B) void k_stream(typename Op::Args a, long long nunits) {
+  const long long tile = (long long)B * K;
   for (long long base = (long long)blockIdx.x * tile; base < nunits;
        base += (long long)gridDim.x * tile) {
     typename Op::In v[K];
     if (base + tile <= nunits) {
 #pragma unroll
-      for (int k = 0; k < K; ++k) v[k] = Op::template load<NT>(a, base + k * kBlock + threadIdx.x);
+      for (int k = 0; k < K; ++k) v[k] = Op::template load<NT>(a, base + k * B + threadIdx.x);
 #pragma unroll
-      for (int k = 0; k < K; ++k) Op::template apply<NT>(a, base + k * kBlock + threadIdx.x, v[k]);
+      for (int k = 0; k < K; ++k) Op::template apply<NT>(a, base + k * B + threadIdx.x, v[k]);
     } else {
 #pragma unroll
       for (int k = 0; k < K; ++k) {
-        const long long u = base + k * kBlock + threadIdx.x;
+        const long long u = base + k * B + threadIdx.x;
         if (u < nunits) v[k] = Op::template load<NT>(a, u);
       }
 #pragma unroll
       for (int k = 0; k < K; ++k) {
-        const long long u = base + k * kBlock + threadIdx.x;
+        const long long u = base + k * B + threadIdx.x;
         if (u < nunits) Op::template apply<NT>(a, u, v[k]);
       }
     }
@@ -298,7 +298,7 @@ __global__ __launch_bounds__(kBlock) void k_scalar(typename Op::Args a, long lon
 
 // Batched: blockIdx.y = tensor, blockIdx.x = tile of that tensor (one launch for `count`
 // tensors; BASELINE config 3). Arrays of pointers / sizes live in device memory.
-template <class Op, int K>
+template <class Op, int K, int NT>
 __global__ __launch_bounds__(kBlock) void k_batched(const void* const* src, void* const* dst0,
                                                     void* const* dst1, const long long* ns,
                                                     int flag, long long tile_base) {
@@ -321,7 +321,7 @@ __global__ __launch_bounds__(kBlock) void k_batched(const void* const* src, void
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const long long u = u0 + k * kBlock + threadIdx.x;
-      if (u < nunits) Op::template apply<0>(a, u, Op::template load<0>(a, u));
+      if (u < nunits) Op::template apply<NT>(a, u, Op::template load<NT>(a, u));
     }
     // ragged tail (< kElems elements) of this tensor, handled by the tile that owns it
     const long long tail0 = nunits * Op::kElems;
@@ -385,40 +385,62 @@ __global__ __launch_bounds__(kBlock) void k_decode_hex(const char* chars, const 
 // launch configuration (tunable; see efl_fxp_tune)
 // ------------------------------------------------------------------------------------------
 
-std::atomic<int> g_enc_variant{0};   // 0 pair, 1 quad
-std::atomic<int> g_dec_variant{0};   // 0 pair, 1 quad
-std::atomic<int> g_tiles{4};         // K: units per lane per tile (1, 2, 4)
-std::atomic<int> g_grid_cap{0};      // 0: one tile per workgroup; else max workgroups
-std::atomic<int> g_nt{0};            // 0 none, 2 nt stores, 3 nt loads+stores
+// Per-direction launch shape of the fp32 kernels. Defaults: the fastest of the interleaved
+// variant sweep on MI355X (tools/sweep_fxp.py, profiles/). Encode (4 B in, 16 B out) prefers
+// plain stores; decode (16 B in, 4 B out) gains from nontemporal loads+stores.
+struct Shape {
+  std::atomic<int> variant;   // 0 pair, 1 quad
+  std::atomic<int> block;     // 128, 256, 512
+  std::atomic<int> k;         // units per lane per tile: 1, 2
+  std::atomic<int> nt;        // bit0 nontemporal loads, bit1 nontemporal stores
+};
+Shape g_shape[2] = {{{0}, {256}, {1}, {0}}, {{0}, {256}, {1}, {3}}};
+std::atomic<int> g_grid_cap{0};   // 0: one tile per workgroup; else max workgroups
+constexpr int kEnc = 0, kDec = 1;
 
-template <class Op, int K, int NT>
+template <class Op, int B, int K, int NT>
 hipError_t launch_k(const typename Op::Args& a, long long nunits, hipStream_t s) {
-  const long long tile = (long long)kBlock * K;
+  const long long tile = (long long)B * K;
   long long grid = (nunits + tile - 1) / tile;
   const int cap = g_grid_cap.load(std::memory_order_relaxed);
   if (cap > 0 && grid > cap) grid = cap;
   if (grid > 0x7FFFFFFFll) grid = 0x7FFFFFFFll;
   if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL((k_stream<Op, K, NT>), dim3((unsigned)grid), dim3(kBlock), 0, s, a, nunits);
+  hipLaunchKernelGGL((k_stream<Op, B, K, NT>), dim3((unsigned)grid), dim3(B), 0, s, a, nunits);
   return hipGetLastError();
 }
 
-template <class Op, int K>
-hipError_t launch_nt(const typename Op::Args& a, long long nunits, hipStream_t s) {
-  switch (g_nt.load(std::memory_order_relaxed)) {
-    case 2: return launch_k<Op, K, 2>(a, nunits, s);
-    case 3: return launch_k<Op, K, 3>(a, nunits, s);
-    default: return launch_k<Op, K, 0>(a, nunits, s);
+template <class Op, int B, int K>
+hipError_t launch_nt(int nt, const typename Op::Args& a, long long nunits, hipStream_t s) {
+  switch (nt) {
+    case 1: return launch_k<Op, B, K, 1>(a, nunits, s);
+    case 2: return launch_k<Op, B, K, 2>(a, nunits, s);
+    case 3: return launch_k<Op, B, K, 3>(a, nunits, s);
+    default: return launch_k<Op, B, K, 0>(a, nunits, s);
   }
 }
 
+template <class Op, int B>
+hipError_t launch_bk(const Shape& sh, const typename Op::Args& a, long long nunits, hipStream_t s) {
+  const int nt = sh.nt.load(std::memory_order_relaxed);
+  return sh.k.load(std::memory_order_relaxed) == 2 ? launch_nt<Op, B, 2>(nt, a, nunits, s)
+                                                   : launch_nt<Op, B, 1>(nt, a, nunits, s);
+}
+
+// tunable launch (fp32 ops)
 template <class Op>
-hipError_t launch_stream(const typename Op::Args& a, long long nunits, hipStream_t s) {
-  switch (g_tiles.load(std::memory_order_relaxed)) {
-    case 1: return launch_nt<Op, 1>(a, nunits, s);
-    case 2: return launch_nt<Op, 2>(a, nunits, s);
-    default: return launch_nt<Op, 4>(a, nunits, s);
+hipError_t launch_tuned(const Shape& sh, const typename Op::Args& a, long long nunits, hipStream_t s) {
+  switch (sh.block.load(std::memory_order_relaxed)) {
+    case 128: return launch_bk<Op, 128>(sh, a, nunits, s);
+    case 512: return launch_bk<Op, 512>(sh, a, nunits, s);
+    default: return launch_bk<Op, 256>(sh, a, nunits, s);
   }
+}
+
+// fixed launch (fp64 / integer ops): the fp32 defaults of the same direction
+template <class Op>
+hipError_t launch_fixed(int dir, const typename Op::Args& a, long long nunits, hipStream_t s) {
+  return dir == kEnc ? launch_k<Op, 256, 1, 0>(a, nunits, s) : launch_k<Op, 256, 1, 3>(a, nunits, s);
 }
 
 template <class Op>
@@ -431,13 +453,14 @@ hipError_t launch_scalar(const typename Op::Args& a, long long start, long long 
 }
 
 // vector path over the aligned prefix + scalar tail, or all-scalar when unaligned.
-template <class Op>
-hipError_t run(const typename Op::Args& a, const void* p0, const void* p1, const void* p2,
+template <class Op, bool TUNED>
+hipError_t run(int dir, const typename Op::Args& a, const void* p0, const void* p1, const void* p2,
                long long n, hipStream_t s) {
   const uintptr_t need = 16;
   if (aligned(p0, need) && aligned(p1, need) && aligned(p2, need)) {
     const long long nunits = n / Op::kElems;
-    hipError_t e = launch_stream<Op>(a, nunits, s);
+    hipError_t e = TUNED ? launch_tuned<Op>(g_shape[dir], a, nunits, s)
+                         : launch_fixed<Op>(dir, a, nunits, s);
     if (e != hipSuccess) return e;
     return launch_scalar<Op>(a, nunits * Op::kElems, n, s);
   }
@@ -478,16 +501,26 @@ EFL_API const char* efl_version(void) { return "efl-hip 0.1.0 (gfx950)"; }
 EFL_API const char* efl_last_error(void) { return t_err.c_str(); }
 
 EFL_API int efl_fxp_tune(int kind, int value) {
-  std::atomic<int>* slot = nullptr;
-  switch (kind) {
-    case 0: if (value < 0 || value > 1) return EFL_E_INVALID_ARGUMENT; slot = &g_enc_variant; break;
-    case 1: if (value < 0 || value > 1) return EFL_E_INVALID_ARGUMENT; slot = &g_dec_variant; break;
-    case 2: if (value != 1 && value != 2 && value != 4) return EFL_E_INVALID_ARGUMENT; slot = &g_tiles; break;
-    case 3: if (value < 0) return EFL_E_INVALID_ARGUMENT; slot = &g_grid_cap; break;
-    case 4: if (value != 0 && value != 2 && value != 3) return EFL_E_INVALID_ARGUMENT; slot = &g_nt; break;
-    default: return EFL_E_INVALID_ARGUMENT;
+  if (kind == 8) {
+    if (value < 0) return EFL_E_INVALID_ARGUMENT;
+    return g_grid_cap.exchange(value);
   }
-  return slot->exchange(value);
+  if (kind < 0 || kind > 7) return EFL_E_INVALID_ARGUMENT;
+  Shape& sh = g_shape[kind & 1];
+  switch (kind >> 1) {
+    case 0:
+      if (value < 0 || value > 1) return EFL_E_INVALID_ARGUMENT;
+      return sh.variant.exchange(value);
+    case 1:
+      if (value != 1 && value != 2) return EFL_E_INVALID_ARGUMENT;
+      return sh.k.exchange(value);
+    case 2:
+      if (value < 0 || value > 3) return EFL_E_INVALID_ARGUMENT;
+      return sh.nt.exchange(value);
+    default:
+      if (value != 128 && value != 256 && value != 512) return EFL_E_INVALID_ARGUMENT;
+      return sh.block.exchange(value);
+  }
 }
 
 EFL_API int efl_fxp_encode(const void* x, int dtype, int64_t* mantissa, int64_t* exponent,
@@ -500,14 +533,14 @@ EFL_API int efl_fxp_encode(const void* x, int dtype, int64_t* mantissa, int64_t*
   hipError_t e;
   switch (dtype) {
     case EFL_DT_FLOAT:
-      e = g_enc_variant.load() == 1 ? run<EncF32Quad>(a, x, mantissa, exponent, n, s)
-                                    : run<EncF32Pair>(a, x, mantissa, exponent, n, s);
+      e = g_shape[kEnc].variant.load() == 1 ? run<EncF32Quad, true>(kEnc, a, x, mantissa, exponent, n, s)
+                                            : run<EncF32Pair, true>(kEnc, a, x, mantissa, exponent, n, s);
       break;
-    case EFL_DT_DOUBLE: e = run<EncF64Pair>(a, x, mantissa, exponent, n, s); break;
-    case EFL_DT_INT8: e = run<EncIntPair<signed char, c2>>(a, x, mantissa, exponent, n, s); break;
-    case EFL_DT_INT16: e = run<EncIntPair<short, s2>>(a, x, mantissa, exponent, n, s); break;
-    case EFL_DT_INT32: e = run<EncIntPair<int, i2>>(a, x, mantissa, exponent, n, s); break;
-    case EFL_DT_INT64: e = run<EncIntPair<long long, ll2>>(a, x, mantissa, exponent, n, s); break;
+    case EFL_DT_DOUBLE: e = run<EncF64Pair, false>(kEnc, a, x, mantissa, exponent, n, s); break;
+    case EFL_DT_INT8: e = run<EncIntPair<signed char, c2>, false>(kEnc, a, x, mantissa, exponent, n, s); break;
+    case EFL_DT_INT16: e = run<EncIntPair<short, s2>, false>(kEnc, a, x, mantissa, exponent, n, s); break;
+    case EFL_DT_INT32: e = run<EncIntPair<int, i2>, false>(kEnc, a, x, mantissa, exponent, n, s); break;
+    case EFL_DT_INT64: e = run<EncIntPair<long long, ll2>, false>(kEnc, a, x, mantissa, exponent, n, s); break;
     default:
       set_error("ConvertToFixedPoint: unsupported dtype %d (int8/16/32/64, float, double)", dtype);
       return EFL_E_INVALID_ARGUMENT;
@@ -530,10 +563,10 @@ EFL_API int efl_fxp_decode(const int64_t* mantissa, const int64_t* exponent, voi
   hipError_t e;
   switch (dtype) {
     case EFL_DT_FLOAT:
-      e = g_dec_variant.load() == 1 ? run<DecF32Quad>(a, mantissa, exponent, y, n, s)
-                                    : run<DecF32Pair>(a, mantissa, exponent, y, n, s);
+      e = g_shape[kDec].variant.load() == 1 ? run<DecF32Quad, true>(kDec, a, mantissa, exponent, y, n, s)
+                                            : run<DecF32Pair, true>(kDec, a, mantissa, exponent, y, n, s);
       break;
-    case EFL_DT_DOUBLE: e = run<DecF64Pair>(a, mantissa, exponent, y, n, s); break;
+    case EFL_DT_DOUBLE: e = run<DecF64Pair, false>(kDec, a, mantissa, exponent, y, n, s); break;
     default:
       set_error("FixedPointToFloatPoint: unsupported dtype %d (float, double)", dtype);
       return EFL_E_INVALID_ARGUMENT;
@@ -570,7 +603,7 @@ namespace {
 constexpr int kBatchK = 4;
 constexpr long long kMaxGridY = 65535;
 
-template <class Op>
+template <class Op, int NT>
 hipError_t launch_batched(const void* const* src, void* const* d0, void* const* d1,
                           const long long* ns, long long count, long long max_n, int flag,
                           hipStream_t s) {
@@ -579,7 +612,7 @@ hipError_t launch_batched(const void* const* src, void* const* d0, void* const* 
   if (gx == 0 || count == 0) return hipSuccess;
   for (long long b = 0; b < count; b += kMaxGridY) {
     const long long gy = count - b < kMaxGridY ? count - b : kMaxGridY;
-    hipLaunchKernelGGL((k_batched<Op, kBatchK>), dim3((unsigned)gx, (unsigned)gy), dim3(kBlock), 0, s,
+    hipLaunchKernelGGL((k_batched<Op, kBatchK, NT>), dim3((unsigned)gx, (unsigned)gy), dim3(kBlock), 0, s,
                        src, d0, d1, ns, flag, b);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -600,12 +633,12 @@ EFL_API int efl_fxp_encode_batched(const void* const* xs, int dtype, int64_t* co
   const int f = decrease_precision ? 1 : 0;
   hipError_t e;
   switch (dtype) {
-    case EFL_DT_FLOAT: e = launch_batched<EncF32Pair>(xs, d0, d1, nn, count, max_n, f, s); break;
-    case EFL_DT_DOUBLE: e = launch_batched<EncF64Pair>(xs, d0, d1, nn, count, max_n, f, s); break;
-    case EFL_DT_INT8: e = launch_batched<EncIntPair<signed char, c2>>(xs, d0, d1, nn, count, max_n, f, s); break;
-    case EFL_DT_INT16: e = launch_batched<EncIntPair<short, s2>>(xs, d0, d1, nn, count, max_n, f, s); break;
-    case EFL_DT_INT32: e = launch_batched<EncIntPair<int, i2>>(xs, d0, d1, nn, count, max_n, f, s); break;
-    case EFL_DT_INT64: e = launch_batched<EncIntPair<long long, ll2>>(xs, d0, d1, nn, count, max_n, f, s); break;
+    case EFL_DT_FLOAT: e = launch_batched<EncF32Pair, 0>(xs, d0, d1, nn, count, max_n, f, s); break;
+    case EFL_DT_DOUBLE: e = launch_batched<EncF64Pair, 0>(xs, d0, d1, nn, count, max_n, f, s); break;
+    case EFL_DT_INT8: e = launch_batched<EncIntPair<signed char, c2>, 0>(xs, d0, d1, nn, count, max_n, f, s); break;
+    case EFL_DT_INT16: e = launch_batched<EncIntPair<short, s2>, 0>(xs, d0, d1, nn, count, max_n, f, s); break;
+    case EFL_DT_INT32: e = launch_batched<EncIntPair<int, i2>, 0>(xs, d0, d1, nn, count, max_n, f, s); break;
+    case EFL_DT_INT64: e = launch_batched<EncIntPair<long long, ll2>, 0>(xs, d0, d1, nn, count, max_n, f, s); break;
     default:
       set_error("ConvertToFixedPoint: unsupported dtype %d", dtype);
       return EFL_E_INVALID_ARGUMENT;
@@ -624,8 +657,8 @@ EFL_API int efl_fxp_decode_batched(const int64_t* const* mantissas, const int64_
   auto nn = (const long long*)ns;
   hipError_t e;
   switch (dtype) {
-    case EFL_DT_FLOAT: e = launch_batched<DecF32Pair>(src, d0, ys, nn, count, max_n, flags, s); break;
-    case EFL_DT_DOUBLE: e = launch_batched<DecF64Pair>(src, d0, ys, nn, count, max_n, flags, s); break;
+    case EFL_DT_FLOAT: e = launch_batched<DecF32Pair, 3>(src, d0, ys, nn, count, max_n, flags, s); break;
+    case EFL_DT_DOUBLE: e = launch_batched<DecF64Pair, 3>(src, d0, ys, nn, count, max_n, flags, s); break;
     default:
       set_error("FixedPointToFloatPoint: unsupported dtype %d", dtype);
       return EFL_E_INVALID_ARGUMENT;

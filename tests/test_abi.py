@@ -54,6 +54,7 @@ def test_argument_errors_without_gpu():
     assert lib.efl_fxp_encode(ctypes.c_void_p(16), 7, ctypes.c_void_p(16), ctypes.c_void_p(16), 5, 0, None) == -3
     assert "unsupported dtype" in lib.efl_last_error().decode()
     assert lib.efl_fxp_tune(2, 3) == -3
+    assert lib.efl_fxp_tune(9, 0) == -3
     prev = lib.efl_fxp_tune(2, 2)
     assert lib.efl_fxp_tune(2, prev) == 2
 

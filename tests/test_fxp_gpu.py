@@ -185,7 +185,7 @@ def test_errors(efl):
                                                torch.int32)
 
 
-@pytest.mark.parametrize("knob", [(0, 1), (1, 1), (2, 1), (2, 2), (3, 512), (4, 2), (4, 3)])
+@pytest.mark.parametrize("knob", [(0, 1), (1, 1), (2, 2), (3, 2), (4, 1), (5, 0), (4, 3), (6, 128), (7, 512), (8, 512)])
 def test_tuning_variants_identical(efl, knob):
     lib = efl.lib.raw()
     n = (1 << 18) + 7

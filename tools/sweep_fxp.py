@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
-"""Stage-F kernel variant sweep on the bench workload (256 MiB fp32), interleaved rounds in ONE
-process (cdna_hip_programming.md §5.4 rule 24). Prints per-variant median/min kernel times and the
-achieved algorithmic GB/s. Knobs: efl_fxp_tune kinds 0 enc variant, 1 dec variant, 2 K, 3 grid
-cap, 4 NT mode."""
+"""Stage-F launch-shape sweep on the bench workload (256 MiB fp32), interleaved rounds in ONE
+process (cdna_hip_programming.md §5.4 rule 24). Each direction is swept with the other at its
+default. Prints per-shape median/min kernel time and achieved algorithmic GB/s (20 B/element).
+efl_fxp_tune kind = 2*field + dir: field 0 layout, 1 K, 2 NT mask, 3 block; kind 8 grid cap."""
 import itertools
 import json
 import os
@@ -24,45 +24,50 @@ E = torch.empty(n, dtype=torch.int64, device=dev)
 y = torch.empty_like(x)
 s = torch.cuda.current_stream()
 sh = s.cuda_stream
+DEFAULT = {d: {f: lib.efl_fxp_tune(2 * f + d, v) for f, v in ((0, 0), (1, 1), (2, 0), (3, 256))} for d in (0, 1)}
+for d in (0, 1):
+    for f, v in DEFAULT[d].items():
+        lib.efl_fxp_tune(2 * f + d, v)
+shapes = [dict(layout=l, K=k, nt=t, block=b) for l, k, t, b in
+          itertools.product((0, 1), (1, 2), (0, 1, 2, 3), (128, 256, 512))]
+rounds = int(os.environ.get("SWEEP_ROUNDS", "4"))
+reps = 3
 
-variants = []
-for var, K, cap, nt in itertools.product((0, 1), (1, 2, 4), (0, 2048), (0, 2, 3)):
-    variants.append({"var": var, "K": K, "cap": cap, "nt": nt})
-rounds = int(os.environ.get("SWEEP_ROUNDS", "5"))
-reps = 4
-res = {i: {"enc": [], "dec": []} for i in range(len(variants))}
+
+def apply(d, shp):
+    for f, key in ((0, "layout"), (1, "K"), (2, "nt"), (3, "block")):
+        assert lib.efl_fxp_tune(2 * f + d, shp[key]) >= 0
 
 
-def setv(v):
-    for kind, val in ((0, v["var"]), (1, v["var"]), (2, v["K"]), (3, v["cap"]), (4, v["nt"])):
-        assert lib.efl_fxp_tune(kind, val) >= 0
+def restore(d):
+    for f, v in DEFAULT[d].items():
+        lib.efl_fxp_tune(2 * f + d, v)
 
 
 ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+res = {(d, i): [] for d in (0, 1) for i in range(len(shapes))}
 for r in range(rounds):
-    for i, v in enumerate(variants):
-        setv(v)
-        for _ in range(reps + 1):
-            ev[0].record(s)
-            efl.lib.check(lib.efl_fxp_encode(x.data_ptr(), 1, M.data_ptr(), E.data_ptr(), n, 0, sh))
-            ev[1].record(s)
-            efl.lib.check(lib.efl_fxp_decode(M.data_ptr(), E.data_ptr(), y.data_ptr(), 1, n, n, 0, sh))
-            ev[2].record(s)
-            torch.cuda.synchronize()
-            if _ == 0:
-                continue   # first launch after a switch: warm
-            res[i]["enc"].append(ev[0].elapsed_time(ev[1]))
-            res[i]["dec"].append(ev[1].elapsed_time(ev[2]))
+    for d in (0, 1):
+        for i, shp in enumerate(shapes):
+            apply(d, shp)
+            for j in range(reps + 1):
+                ev[0].record(s)
+                efl.lib.check(lib.efl_fxp_encode(x.data_ptr(), 1, M.data_ptr(), E.data_ptr(), n, 0, sh))
+                ev[1].record(s)
+                efl.lib.check(lib.efl_fxp_decode(M.data_ptr(), E.data_ptr(), y.data_ptr(), 1, n, n, 0, sh))
+                ev[2].record(s)
+                torch.cuda.synchronize()
+                if j:
+                    res[(d, i)].append(ev[d].elapsed_time(ev[d + 1]))
+            restore(d)
     nz = x != 0
     assert torch.equal(y[nz], x[nz])
 
-rows = []
-for i, v in enumerate(variants):
-    e, d = np.array(res[i]["enc"]), np.array(res[i]["dec"])
-    rows.append(dict(v, enc_med=float(np.median(e)), enc_min=float(e.min()),
-                     dec_med=float(np.median(d)), dec_min=float(d.min()),
-                     enc_GBs=20 * n / (np.median(e) * 1e-3) / 1e9,
-                     dec_GBs=20 * n / (np.median(d) * 1e-3) / 1e9))
-rows.sort(key=lambda r: r["enc_med"] + r["dec_med"])
-for r in rows:
+out = []
+for (d, i), t in res.items():
+    t = np.array(t)
+    out.append(dict(dir="encode" if d == 0 else "decode", **shapes[i], med_ms=float(np.median(t)),
+                    min_ms=float(t.min()), GBs=20 * n / (np.median(t) * 1e-3) / 1e9))
+out.sort(key=lambda r: (r["dir"], r["med_ms"]))
+for r in out:
     print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}))
