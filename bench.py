@@ -64,18 +64,17 @@ def setup_dist(args):
     return world, rank, local
 
 
-def broadcast_seed(world, rank, dev):
-    """RCCL broadcast of the 32-byte key seed over xGMI (the path's only collective)."""
-    seed = torch.zeros(32, dtype=torch.uint8, device=dev)
-    if rank == 0:
-        seed.copy_(torch.from_numpy(np.frombuffer(os.urandom(32), np.uint8).copy()))
+def broadcast_seed(world, rank):
+    """RCCL broadcast of the key material (32-byte seed) from rank 0 over xGMI — the path's only
+    collective (efl.distributed.broadcast_key_material); timed apart from the steps."""
     if world == 1:
-        return seed, 0.0
-    dist.broadcast(seed, 0)                     # warm the communicator
+        return os.urandom(32), 0.0
+    from efl import distributed as edist
+    seed, _ = edist.broadcast_key_material()          # warm the communicator
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(10):
-        dist.broadcast(seed, 0)
+        seed, _ = edist.broadcast_key_material(seed if rank == 0 else None)
     torch.cuda.synchronize()
     return seed, (time.perf_counter() - t0) / 10 * 1e6
 
@@ -117,7 +116,7 @@ def main():
         k, v = (int(s) for s in kv.split("="))
         efl.lib.check(min(0, lib.efl_fxp_tune(k, v)))
 
-    seed, bcast_us = broadcast_seed(world, rank, dev)
+    seed, bcast_us = broadcast_seed(world, rank)
     n = args.rows * COLS
     g = torch.Generator(device=dev).manual_seed(rank)
     x = torch.randn(args.rows, COLS, device=dev, generator=g)

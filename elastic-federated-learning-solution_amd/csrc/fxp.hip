@@ -385,16 +385,17 @@ __global__ __launch_bounds__(kBlock) void k_decode_hex(const char* chars, const 
 // launch configuration (tunable; see efl_fxp_tune)
 // ------------------------------------------------------------------------------------------
 
-// Per-direction launch shape of the fp32 kernels. Defaults: the fastest of the interleaved
-// variant sweep on MI355X (tools/sweep_fxp.py, profiles/). Encode (4 B in, 16 B out) prefers
-// plain stores; decode (16 B in, 4 B out) gains from nontemporal loads+stores.
+// Per-direction launch shape of the fp32 kernels. Defaults: the fastest shape of the interleaved
+// sweep on MI355X (tools/sweep_fxp.py -> profiles/r01/sweep_shapes.jsonl): pair layout, one tile
+// of 128 lanes per workgroup, nontemporal LOADS (the once-read stream), plain stores. Plain vs
+// nontemporal stores were within noise for encode; nontemporal loads gained ~5 % on decode.
 struct Shape {
   std::atomic<int> variant;   // 0 pair, 1 quad
   std::atomic<int> block;     // 128, 256, 512
   std::atomic<int> k;         // units per lane per tile: 1, 2
   std::atomic<int> nt;        // bit0 nontemporal loads, bit1 nontemporal stores
 };
-Shape g_shape[2] = {{{0}, {256}, {1}, {0}}, {{0}, {256}, {1}, {3}}};
+Shape g_shape[2] = {{{0}, {128}, {1}, {1}}, {{0}, {128}, {1}, {1}}};
 std::atomic<int> g_grid_cap{0};   // 0: one tile per workgroup; else max workgroups
 constexpr int kEnc = 0, kDec = 1;
 
@@ -440,7 +441,8 @@ hipError_t launch_tuned(const Shape& sh, const typename Op::Args& a, long long n
 // fixed launch (fp64 / integer ops): the fp32 defaults of the same direction
 template <class Op>
 hipError_t launch_fixed(int dir, const typename Op::Args& a, long long nunits, hipStream_t s) {
-  return dir == kEnc ? launch_k<Op, 256, 1, 0>(a, nunits, s) : launch_k<Op, 256, 1, 3>(a, nunits, s);
+  (void)dir;
+  return launch_k<Op, 128, 1, 1>(a, nunits, s);
 }
 
 template <class Op>
@@ -633,12 +635,12 @@ EFL_API int efl_fxp_encode_batched(const void* const* xs, int dtype, int64_t* co
   const int f = decrease_precision ? 1 : 0;
   hipError_t e;
   switch (dtype) {
-    case EFL_DT_FLOAT: e = launch_batched<EncF32Pair, 0>(xs, d0, d1, nn, count, max_n, f, s); break;
-    case EFL_DT_DOUBLE: e = launch_batched<EncF64Pair, 0>(xs, d0, d1, nn, count, max_n, f, s); break;
-    case EFL_DT_INT8: e = launch_batched<EncIntPair<signed char, c2>, 0>(xs, d0, d1, nn, count, max_n, f, s); break;
-    case EFL_DT_INT16: e = launch_batched<EncIntPair<short, s2>, 0>(xs, d0, d1, nn, count, max_n, f, s); break;
-    case EFL_DT_INT32: e = launch_batched<EncIntPair<int, i2>, 0>(xs, d0, d1, nn, count, max_n, f, s); break;
-    case EFL_DT_INT64: e = launch_batched<EncIntPair<long long, ll2>, 0>(xs, d0, d1, nn, count, max_n, f, s); break;
+    case EFL_DT_FLOAT: e = launch_batched<EncF32Pair, 1>(xs, d0, d1, nn, count, max_n, f, s); break;
+    case EFL_DT_DOUBLE: e = launch_batched<EncF64Pair, 1>(xs, d0, d1, nn, count, max_n, f, s); break;
+    case EFL_DT_INT8: e = launch_batched<EncIntPair<signed char, c2>, 1>(xs, d0, d1, nn, count, max_n, f, s); break;
+    case EFL_DT_INT16: e = launch_batched<EncIntPair<short, s2>, 1>(xs, d0, d1, nn, count, max_n, f, s); break;
+    case EFL_DT_INT32: e = launch_batched<EncIntPair<int, i2>, 1>(xs, d0, d1, nn, count, max_n, f, s); break;
+    case EFL_DT_INT64: e = launch_batched<EncIntPair<long long, ll2>, 1>(xs, d0, d1, nn, count, max_n, f, s); break;
     default:
       set_error("ConvertToFixedPoint: unsupported dtype %d", dtype);
       return EFL_E_INVALID_ARGUMENT;
@@ -657,8 +659,8 @@ EFL_API int efl_fxp_decode_batched(const int64_t* const* mantissas, const int64_
   auto nn = (const long long*)ns;
   hipError_t e;
   switch (dtype) {
-    case EFL_DT_FLOAT: e = launch_batched<DecF32Pair, 3>(src, d0, ys, nn, count, max_n, flags, s); break;
-    case EFL_DT_DOUBLE: e = launch_batched<DecF64Pair, 3>(src, d0, ys, nn, count, max_n, flags, s); break;
+    case EFL_DT_FLOAT: e = launch_batched<DecF32Pair, 1>(src, d0, ys, nn, count, max_n, flags, s); break;
+    case EFL_DT_DOUBLE: e = launch_batched<DecF64Pair, 1>(src, d0, ys, nn, count, max_n, flags, s); break;
     default:
       set_error("FixedPointToFloatPoint: unsupported dtype %d", dtype);
       return EFL_E_INVALID_ARGUMENT;

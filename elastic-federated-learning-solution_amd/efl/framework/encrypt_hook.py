@@ -1,0 +1,123 @@
+"""Pre-send / post-recv hook that applies the forward-encryption codec on the MI355X.
+
+The reference's forward path (efls-train/python/efl/privacy/paillier_layer.py:64-67) encodes the
+activation, encrypts the mantissa and sends two tensors, '<p>_[x]_mantissa' and '<p>_[x]_exponent';
+the receiving side recv()s both (paillier_layer.py:121, 188). FixedPointHook packages the Stage-F
+part of that pattern as a Communicator hook so existing send/recv callers need no change:
+
+  send(name, float_tensor)  ->  H2D (if host) -> ConvertToFixedPoint on GPU -> D2H into pinned
+                                 buffers -> send(name+'_mantissa', int64) + send(name+'_exponent', int64)
+  recv(name, dtype=float)   ->  recv both -> H2D -> FixedPointToFloatPoint on GPU -> tensor
+
+The codec functions are injectable (`encode=`, `decode=`) so CPU-only tests can run the same
+plumbing with a CPU checker; by default they are the libefl_hip.so ops (no CPU fallback).
+"""
+from __future__ import annotations
+
+import re
+import time
+
+import torch
+
+from efl import exporter
+from efl.framework.communicator import TensorHook
+
+_FLOATS = (torch.float32, torch.float64)
+
+
+class _PinnedPool:
+    """Reusable page-locked host buffers for the D2H legs (keyed by dtype and size)."""
+
+    def __init__(self):
+        self._bufs = {}
+
+    def get(self, like: torch.Tensor, slot: str) -> torch.Tensor:
+        k = (slot, like.dtype, like.numel())
+        b = self._bufs.get(k)
+        if b is None:
+            b = torch.empty(like.numel(), dtype=like.dtype, pin_memory=torch.cuda.is_available())
+            self._bufs[k] = b
+        return b.view(like.shape)
+
+
+@exporter.export("privacy.FixedPointHook")
+class FixedPointHook(TensorHook):
+    def __init__(self, names=None, decrease_precision=False, return_device=None, encode=None,
+                 decode=None, reuse_buffers=False, stats=None):
+        """names: regex of logical tensor names to transform (default: every float tensor).
+        return_device: where recv() returns the decoded tensor (default: host, like the
+        reference's recv). reuse_buffers: keep pinned D2H buffers across sends (the caller must
+        not send the same name again before the previous send completed). stats: a dict that
+        receives per-stage wall times in seconds (adds device synchronisations; measurement only)."""
+        self.stats = stats
+        self._names = re.compile(names) if names else None
+        self._dp = decrease_precision
+        self._return_device = return_device
+        if encode is None or decode is None:
+            from efl.lib import ops
+            encode = encode or ops.convert_to_fixed_point
+            decode = decode or ops.fixed_point_to_float_point
+        self._encode, self._decode = encode, decode
+        self._pool = _PinnedPool() if reuse_buffers else None
+
+    def _match(self, name):
+        return self._names is None or self._names.search(name) is not None
+
+    def _to_host(self, t: torch.Tensor, slot: str) -> torch.Tensor:
+        if not t.is_cuda:
+            return t
+        if self._pool is not None:
+            h = self._pool.get(t, slot)
+        else:
+            h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+        h.copy_(t, non_blocking=True)
+        return h
+
+    def pre_send(self, name, tensor):
+        if not isinstance(tensor, torch.Tensor) or tensor.dtype not in _FLOATS or not self._match(name):
+            return None
+        t = self._tick()
+        if self.stats is not None and not tensor.is_cuda and torch.cuda.is_available():
+            tensor = tensor.cuda(non_blocking=tensor.is_pinned())
+            t = self._tick("send_h2d", t)
+        M, E = self._encode(tensor, decrease_precision=self._dp)
+        t = self._tick("send_encode", t)
+        Mh, Eh = self._to_host(M, name + "_m"), self._to_host(E, name + "_e")
+        if M.is_cuda:
+            torch.cuda.current_stream(M.device).synchronize()
+        self._tick("send_d2h", t)
+        return [(name + "_mantissa", Mh), (name + "_exponent", Eh)]
+
+    def _tick(self, stage=None, t0=None):
+        if self.stats is None:
+            return None
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        now = time.perf_counter()
+        if stage is not None:
+            self.stats[stage] = self.stats.get(stage, 0.0) + (now - t0)
+        return now
+
+    def post_recv(self, name, shape, dtype, raw_recv):
+        from efl.lib import to_torch_dtype
+        dt = to_torch_dtype(dtype)
+        if dt not in _FLOATS or not self._match(name):
+            return None
+        t = self._tick()
+        M = raw_recv(name + "_mantissa")
+        E = raw_recv(name + "_exponent")
+        t = self._tick("recv_grpc", t)
+        if torch.cuda.is_available():
+            M = M.cuda() if not M.is_cuda else M
+            E = E.cuda() if not E.is_cuda else E
+        t = self._tick("recv_h2d", t)
+        y = self._decode(M, E, dt)
+        t = self._tick("recv_decode", t)
+        if shape is not None:
+            y = y.reshape(tuple(int(s) for s in shape))
+        if self._return_device is not None:
+            y = y.to(self._return_device)
+        elif y.is_cuda:
+            y = y.cpu()
+        self._tick("recv_d2h", t)
+        return y

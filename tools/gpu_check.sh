@@ -9,7 +9,7 @@ mkdir -p $O
 STAGE=${1:-all}
 run_tests() { timeout -k 10 900 python -m pytest tests -m gpu -x -q > $O/pytest_gpu.log 2>&1; }
 run_smoke() { timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1; }
-run_bench() { timeout -k 10 300 python bench.py --steps 50 --warmup 5 > $O/bench.json 2> $O/bench.err && timeout -k 10 300 python tools/bench_batched.py > $O/bench_batched.json 2> $O/bench_batched.err; }
+run_bench() { timeout -k 10 300 python bench.py --steps 50 --warmup 5 > $O/bench.json 2> $O/bench.err && timeout -k 10 300 python tools/bench_batched.py > $O/bench_batched.json 2> $O/bench_batched.err && timeout -k 10 600 python tools/bench_e2e.py > $O/bench_e2e.json 2> $O/bench_e2e.err; }
 run_sweep() { timeout -k 10 300 python tools/sweep_fxp.py > $O/sweep.jsonl 2> $O/sweep.err; }
 run_prof() {
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_trace -o run --output-format csv \
