@@ -1,0 +1,690 @@
+// Stage P — Paillier cipher of EFLS-train's forward-encryption path on MI355X (gfx950).
+//
+// Reference: efls-train/cc/efl/math/paillier.cc
+//   PaillierKeypair::Encrypt :103-131 (hsa given, or hsa = fbpowm(random a) when "0")
+//   _Decrypt :296-312 with m-function :39-48, h-function :28-37
+//   FixedBasePowm (table + lookup with per-group bit-reversed index) gmp_utils.cc:56-144
+//   Add/MulScalar/MulExp2/Invert :157-285
+//
+// One ciphertext per lane. Big numbers are little-endian 32-bit limbs, element-major in HBM
+// ([N][L]); per lane they live in VGPRs (operand a, accumulator t) and in the lane's LDS column
+// (operand b, stride = workgroup size). Moduli and key constants are wave-uniform (scalar loads).
+// The per-element randomness `a` of hsa = hs^a comes from Philox4x32-10 keyed by the broadcast
+// seed with counter = global element index (counter-based: independent of GPU count/launch shape).
+#include "bignum.h"
+#include "common.h"
+
+namespace efl {
+namespace {
+
+using namespace big;
+
+constexpr int kPlBlock = 64;   // one wave per workgroup: LDS columns are per lane
+
+struct Key {
+  const uint32_t* base;
+  efl_pl_key d;
+  __device__ __forceinline__ const uint32_t* at(int64_t off) const { return base + off; }
+};
+
+// ------------------------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al., SC'11): counter (ctr_lo, ctr_hi, block, 0), key = seed.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void philox(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+    c[0] = n0;
+    c[1] = (uint32_t)p1;
+    c[2] = n2;
+    c[3] = (uint32_t)p0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
+// a = Philox stream of `words` 32-bit words for element counter ctr, written to an LDS column.
+__device__ __forceinline__ void draw_a(uint32_t* col, int S, int words, int a_bits, uint64_t seed,
+                                       uint64_t ctr) {
+  for (int b = 0; b * 4 < words; ++b) {
+    uint32_t c[4] = {(uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)b, 0u};
+    philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (b * 4 + j < words) col[(b * 4 + j) * S] = c[j];
+  }
+  const int rem = a_bits & 31;
+  if (rem) col[(words - 1) * S] &= (1u << rem) - 1u;
+}
+
+// ------------------------------------------------------------------------------------------
+// helpers
+// ------------------------------------------------------------------------------------------
+
+template <int L>
+__device__ __forceinline__ void load_g(uint32_t (&x)[L], const uint32_t* __restrict__ g) {
+#pragma unroll
+  for (int j = 0; j < L; j += 4) {
+    const uint4 v = *reinterpret_cast<const uint4*>(g + j);
+    x[j] = v.x; x[j + 1] = v.y; x[j + 2] = v.z; x[j + 3] = v.w;
+  }
+}
+
+template <int L>
+__device__ __forceinline__ void store_g(uint32_t* __restrict__ g, const uint32_t (&x)[L]) {
+#pragma unroll
+  for (int j = 0; j < L; j += 4) *reinterpret_cast<uint4*>(g + j) = make_uint4(x[j], x[j + 1], x[j + 2], x[j + 3]);
+}
+
+template <int L>
+__device__ __forceinline__ void load_uniform(uint32_t (&x)[L], const uint32_t* __restrict__ g) {
+#pragma unroll
+  for (int j = 0; j < L; ++j) x[j] = g[j];
+}
+
+// copy L limbs from global (per lane) into the lane's LDS column
+template <int L>
+__device__ __forceinline__ void g_to_lds(uint32_t* col, int S, const uint32_t* __restrict__ g) {
+#pragma unroll
+  for (int j = 0; j < L; j += 4) {
+    const uint4 v = *reinterpret_cast<const uint4*>(g + j);
+    col[j * S] = v.x; col[(j + 1) * S] = v.y; col[(j + 2) * S] = v.z; col[(j + 3) * S] = v.w;
+  }
+}
+
+// g = 1 + a*n  (a = |m|, 64-bit) or its inverse mod n^2, 1 - a*n = n^2 + 1 - a*n  (m < 0).
+// paillier.cc:110-124: (1+|m|n)^-1 mod n^2 is exactly n^2 + 1 - |m|n because (1+an)(1-an) = 1 - a^2 n^2.
+template <int LN>
+__device__ __forceinline__ void make_g(uint32_t (&g)[2 * LN], long long m, const uint32_t* __restrict__ n,
+                                       const uint32_t* __restrict__ n2) {
+  constexpr int LC = 2 * LN;
+  const uint64_t a = m < 0 ? 0ull - (uint64_t)m : (uint64_t)m;
+  const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32);
+  // prod = a * n (LN + 2 limbs)
+  uint32_t c0 = 0, c1 = 0;
+#pragma unroll
+  for (int j = 0; j < LC; ++j) g[j] = 0;
+#pragma unroll
+  for (int j = 0; j < LN; ++j) {
+    const uint64_t p = mad(a0, n[j], (uint64_t)g[j] + c0);
+    g[j] = (uint32_t)p;
+    c0 = (uint32_t)(p >> 32);
+  }
+  g[LN] = c0;
+#pragma unroll
+  for (int j = 0; j < LN; ++j) {
+    const uint64_t p = mad(a1, n[j], (uint64_t)g[j + 1] + c1);
+    g[j + 1] = (uint32_t)p;
+    c1 = (uint32_t)(p >> 32);
+  }
+  g[LN + 1] += c1;
+  if (m < 0) {
+    // g = n2 - g + 1
+    uint32_t borrow = 0;
+#pragma unroll
+    for (int j = 0; j < LC; ++j) {
+      const uint64_t d = (uint64_t)n2[j] - g[j] - borrow;
+      g[j] = (uint32_t)d;
+      borrow = (uint32_t)(d >> 63);
+    }
+  }
+  // + 1
+  uint32_t c = 1;
+#pragma unroll
+  for (int j = 0; j < LC; ++j) {
+    const uint64_t s = (uint64_t)g[j] + c;
+    g[j] = (uint32_t)s;
+    c = (uint32_t)(s >> 32);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// fixed-base exponentiation hs^(a') mod n^2 through the table (gmp_utils.cc:107-144):
+// groups of g bits of a, each group's index built MSB-first from its LOW bit; the top partial
+// group likewise. Table entries T[i][j] = hs^((j+1) 2^(g i)) in Montgomery form.
+// Returns acc = hs^(a') * R mod n^2 (Montgomery form).
+// ------------------------------------------------------------------------------------------
+template <int LC>
+__device__ __forceinline__ void fbpowm_mont(uint32_t (&acc)[LC], const Key& k, const uint32_t* acol,
+                                            uint32_t* bcol, int S) {
+  const int g = k.d.group_size;
+  const int words = (k.d.a_bits + 31) >> 5;
+  // bit length of a
+  int size = 0;
+  for (int w = words - 1; w >= 0; --w) {
+    const uint32_t v = acol[w * S];
+    if (v) { size = w * 32 + 32 - __clz(v); break; }
+  }
+  load_uniform<LC>(acc, k.at(k.d.off_n2_one));
+  const uint32_t* n2 = k.at(k.d.off_n2);
+  const uint32_t* table = k.at(k.d.off_table);
+  const int cols = k.d.table_cols;
+  for (int s = 0, row = 0; s < size; s += g, ++row) {
+    const int w = size - s < g ? size - s : g;
+    uint32_t idx = 0;
+    for (int j = 0; j < w; ++j) {
+      const int b = s + j;
+      idx = (idx << 1) | ((acol[(b >> 5) * S] >> (b & 31)) & 1u);
+    }
+    if (idx) {
+      g_to_lds<LC>(bcol, S, table + ((int64_t)row * cols + (idx - 1)) * LC);
+      mont_mul<LC>(acc, LdsCol{bcol, S}, n2, k.d.n2_minv);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// kernels
+// ------------------------------------------------------------------------------------------
+
+// Encrypt (paillier.cc:103-131). hsa: [N][LC] normal-form limbs, or null -> fbpowm of a fresh a.
+template <int LN>
+__global__ __launch_bounds__(kPlBlock) void k_encrypt(Key k, const long long* __restrict__ m,
+                                                      const uint32_t* __restrict__ hsa,
+                                                      uint32_t* __restrict__ out, long long N,
+                                                      uint64_t seed, long long ctr0) {
+  constexpr int LC = 2 * LN;
+  extern __shared__ uint32_t lds[];
+  const int S = blockDim.x;
+  uint32_t* acol = lds + threadIdx.x;
+  uint32_t* bcol = lds + LC * S + threadIdx.x;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const uint32_t* n = k.at(k.d.off_n);
+  const uint32_t* n2 = k.at(k.d.off_n2);
+  uint32_t c[LC];
+  if (hsa) {
+    // c = g * hsa mod n^2 = mont(mont(g, hsa), R^2)
+    make_g<LN>(c, m[i], n, n2);
+    g_to_lds<LC>(bcol, S, hsa + i * LC);
+    mont_mul<LC>(c, LdsCol{bcol, S}, n2, k.d.n2_minv);
+    mont_mul<LC>(c, Uniform{k.at(k.d.off_n2_r2)}, n2, k.d.n2_minv);
+  } else {
+    draw_a(acol, S, (k.d.a_bits + 31) >> 5, k.d.a_bits, seed, (uint64_t)(ctr0 + i));
+    fbpowm_mont<LC>(c, k, acol, bcol, S);      // hs^a' * R
+    to_lds<LC>(bcol, S, c);
+    make_g<LN>(c, m[i], n, n2);
+    mont_mul<LC>(c, LdsCol{bcol, S}, n2, k.d.n2_minv);   // g * hs^a'
+  }
+  store_g<LC>(out + i * LC, c);
+}
+
+// hsa only (hs^a' for a given / drawn a), normal form — exposed for parity with FixedBasePowm.
+template <int LN>
+__global__ __launch_bounds__(kPlBlock) void k_fbpowm(Key k, const uint32_t* __restrict__ a_in,
+                                                     uint32_t* __restrict__ out, long long N,
+                                                     uint64_t seed, long long ctr0) {
+  constexpr int LC = 2 * LN;
+  extern __shared__ uint32_t lds[];
+  const int S = blockDim.x;
+  uint32_t* acol = lds + threadIdx.x;
+  uint32_t* bcol = lds + LC * S + threadIdx.x;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const int words = (k.d.a_bits + 31) >> 5;
+  if (a_in) {
+    for (int w = 0; w < words; ++w) acol[w * S] = a_in[i * words + w];
+  } else {
+    draw_a(acol, S, words, k.d.a_bits, seed, (uint64_t)(ctr0 + i));
+  }
+  uint32_t acc[LC];
+  fbpowm_mont<LC>(acc, k, acol, bcol, S);
+  redc<LC>(acc, k.at(k.d.off_n2), k.d.n2_minv);
+  store_g<LC>(out + i * LC, acc);
+}
+
+// m_x(c) = L_x(c^(x-1) mod x^2) * h mod x   (paillier.cc:39-48), x = p or q.
+// lo/hi: the 2*LP limbs of c (consumed). Result: LH limbs.
+template <int LP>
+__device__ __forceinline__ void m_func(uint32_t (&res)[LP / 2], uint32_t (&lo)[LP], uint32_t (&hi)[LP],
+                                       const Key& k, bool second, uint32_t* acol, uint32_t* bcol, int S) {
+  constexpr int LH = LP / 2;
+  const uint32_t* x2 = k.at(second ? k.d.off_q2 : k.d.off_p2);
+  const uint32_t x2_minv = second ? k.d.q2_minv : k.d.p2_minv;
+  const uint32_t* r3 = k.at(second ? k.d.off_q2_r3 : k.d.off_p2_r3);
+  const uint32_t* e = k.at(second ? k.d.off_qm1 : k.d.off_pm1);
+  const int ebits = second ? k.d.qm1_bits : k.d.pm1_bits;
+  const uint32_t* x = k.at(second ? k.d.off_q : k.d.off_p);
+  const uint32_t x_minv = second ? k.d.q_minv : k.d.p_minv;
+  const uint32_t* xinv_w = k.at(second ? k.d.off_qinv_w : k.d.off_pinv_w);
+  const uint32_t* h_m = k.at(second ? k.d.off_hq : k.d.off_hp);
+
+  redc_wide<LP>(lo, hi, x2, x2_minv);                        // hi = c R^-1 mod x^2
+  mont_mul<LP>(hi, Uniform{r3}, x2, x2_minv);                 // c R mod x^2 (Montgomery form)
+  to_lds<LP>(bcol, S, hi);
+  // left-to-right binary exponentiation by the (uniform) exponent x - 1; top bit is 1
+#pragma unroll 1
+  for (int b = ebits - 2; b >= 0; --b) {
+    mont_sqr<LP>(hi, acol, S, x2, x2_minv);
+    if ((e[b >> 5] >> (b & 31)) & 1u) mont_mul<LP>(hi, LdsCol{bcol, S}, x2, x2_minv);
+  }
+  redc<LP>(hi, x2, x2_minv);                                  // y = c^(x-1) mod x^2
+  const uint32_t (&y)[LP] = hi;
+  // L: (y - 1) / x exactly = (y - 1) * x^-1 mod 2^(32 LH)   (quotient < x)
+  uint32_t y1[LH];
+  uint32_t borrow = 1;
+#pragma unroll
+  for (int j = 0; j < LH; ++j) {
+    const uint64_t d = (uint64_t)y[j] - borrow;
+    y1[j] = (uint32_t)d;
+    borrow = (uint32_t)(d >> 63);
+  }
+  uint32_t q[LH];
+#pragma unroll
+  for (int j = 0; j < LH; ++j) q[j] = 0;
+#pragma unroll
+  for (int i = 0; i < LH; ++i) {
+    uint32_t c = 0;
+    const uint32_t yi = y1[i];
+#pragma unroll
+    for (int j = 0; i + j < LH; ++j) {
+      const uint64_t p = mad(yi, xinv_w[j], (uint64_t)q[i + j] + c);
+      q[i + j] = (uint32_t)p;
+      c = (uint32_t)(p >> 32);
+    }
+  }
+  // * h mod x  (h in Montgomery form -> normal result)
+  mont_mul<LH>(q, Uniform{h_m}, x, x_minv);
+  copy<LH>(res, q);
+}
+
+// Decrypt (paillier.cc:296-312). ct: [N][2LP]; out magnitude [N][LP], neg [N] (1 if m < 0).
+template <int LP>
+__global__ __launch_bounds__(kPlBlock) void k_decrypt(Key k, const uint32_t* __restrict__ ct,
+                                                      uint32_t* __restrict__ mag,
+                                                      signed char* __restrict__ neg, long long N) {
+  constexpr int LH = LP / 2;
+  extern __shared__ uint32_t lds[];
+  const int S = blockDim.x;
+  uint32_t* acol = lds + threadIdx.x;
+  uint32_t* bcol = lds + LP * S + threadIdx.x;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const uint32_t* c = ct + i * 2 * LP;
+  uint32_t lo[LP], hi[LP], mp[LH], mq[LH];
+  load_g<LP>(lo, c);
+  load_g<LP>(hi, c + LP);
+  m_func<LP>(mp, lo, hi, k, false, acol, bcol, S);
+  load_g<LP>(lo, c);
+  load_g<LP>(hi, c + LP);
+  m_func<LP>(mq, lo, hi, k, true, acol, bcol, S);
+  // CRT: m = ((mp - mq) mod p) * (q^-1 mod p) mod p * q + mq
+  const uint32_t* p = k.at(k.d.off_p);
+  const uint32_t* q = k.at(k.d.off_q);
+  uint32_t mqp[LH];
+  copy<LH>(mqp, mq);
+  csub<LH>(mqp, p, geq<LH>(mqp, p));                        // mq < q < 2p
+  uint32_t d[LH];
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int j = 0; j < LH; ++j) {
+    const uint64_t x = (uint64_t)mp[j] - mqp[j] - borrow;
+    d[j] = (uint32_t)x;
+    borrow = (uint32_t)(x >> 63);
+  }
+  if (borrow) {
+    uint32_t c2 = 0;
+#pragma unroll
+    for (int j = 0; j < LH; ++j) {
+      const uint64_t s = (uint64_t)d[j] + p[j] + c2;
+      d[j] = (uint32_t)s;
+      c2 = (uint32_t)(s >> 32);
+    }
+  }
+  mont_mul<LH>(d, Uniform{k.at(k.d.off_qinvp)}, p, k.d.p_minv);
+  const uint32_t (&h)[LH] = d;
+  // m = h * q + mq  (< n)
+  uint32_t m[LP];
+#pragma unroll
+  for (int j = 0; j < LP; ++j) m[j] = j < LH ? mq[j < LH ? j : 0] : 0;
+#pragma unroll
+  for (int a = 0; a < LH; ++a) {
+    uint32_t cc = 0;
+#pragma unroll
+    for (int b = 0; b < LH; ++b) {
+      const uint64_t pr = mad(h[a], q[b], (uint64_t)m[a + b] + cc);
+      m[a + b] = (uint32_t)pr;
+      cc = (uint32_t)(pr >> 32);
+    }
+#pragma unroll
+    for (int b = a + LH; b < LP; ++b) {
+      const uint64_t s = (uint64_t)m[b] + cc;
+      m[b] = (uint32_t)s;
+      cc = (uint32_t)(s >> 32);
+    }
+  }
+  // signed: if m > max (= ceil(2n/3)) then m - n  (paillier.cc:308-310)
+  const uint32_t* mx = k.at(k.d.off_max);
+  uint32_t bb = 0;
+#pragma unroll
+  for (int j = 0; j < LP; ++j) {   // borrow of max - m  -> set iff m > max
+    const uint64_t x = (uint64_t)mx[j] - m[j] - bb;
+    bb = (uint32_t)(x >> 63);
+  }
+  const bool isneg = bb != 0;
+  if (isneg) {   // |m - n| = n - m
+    const uint32_t* n = k.at(k.d.off_n);
+    uint32_t br = 0;
+#pragma unroll
+    for (int j = 0; j < LP; ++j) {
+      const uint64_t x = (uint64_t)n[j] - m[j] - br;
+      m[j] = (uint32_t)x;
+      br = (uint32_t)(x >> 63);
+    }
+  }
+  store_g<LP>(mag + i * LP, m);
+  neg[i] = isneg ? 1 : 0;
+}
+
+// c = x * y mod n^2 (PaillierAdd, paillier.cc:157-178)
+template <int LN>
+__global__ __launch_bounds__(kPlBlock) void k_add(Key k, const uint32_t* __restrict__ x,
+                                                  const uint32_t* __restrict__ y,
+                                                  uint32_t* __restrict__ out, long long N) {
+  constexpr int LC = 2 * LN;
+  extern __shared__ uint32_t lds[];
+  const int S = blockDim.x;
+  uint32_t* bcol = lds + threadIdx.x;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const uint32_t* n2 = k.at(k.d.off_n2);
+  uint32_t a[LC];
+  load_g<LC>(a, x + i * LC);
+  g_to_lds<LC>(bcol, S, y + i * LC);
+  mont_mul<LC>(a, LdsCol{bcol, S}, n2, k.d.n2_minv);
+  mont_mul<LC>(a, Uniform{k.at(k.d.off_n2_r2)}, n2, k.d.n2_minv);
+  store_g<LC>(out + i * LC, a);
+}
+
+// c = x^e mod n^2 for a per-element non-negative exponent of `ewords` 32-bit words
+// (MulScalar / MulExp2, paillier.cc:180-265, 683-719; a negative scalar arrives with x already
+// inverted). exps: [N][ewords].
+template <int LN>
+__global__ __launch_bounds__(kPlBlock) void k_powm(Key k, const uint32_t* __restrict__ x,
+                                                   const uint32_t* __restrict__ exps, int ewords,
+                                                   uint32_t* __restrict__ out, long long N) {
+  constexpr int LC = 2 * LN;
+  extern __shared__ uint32_t lds[];
+  const int S = blockDim.x;
+  uint32_t* acol = lds + threadIdx.x;
+  uint32_t* bcol = lds + LC * S + threadIdx.x;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const uint32_t* n2 = k.at(k.d.off_n2);
+  const uint32_t* e = exps + i * ewords;
+  int ebits = 0;
+  for (int w = ewords - 1; w >= 0; --w)
+    if (e[w]) { ebits = w * 32 + 32 - __clz(e[w]); break; }
+  uint32_t t[LC];
+  if (ebits == 0) {
+    // x^0 = 1 (mpz_powm: 1 mod n^2)
+#pragma unroll
+    for (int j = 0; j < LC; ++j) t[j] = j == 0 ? 1u : 0u;
+    store_g<LC>(out + i * LC, t);
+    return;
+  }
+  load_g<LC>(t, x + i * LC);
+  mont_mul<LC>(t, Uniform{k.at(k.d.off_n2_r2)}, n2, k.d.n2_minv);   // x R
+  to_lds<LC>(bcol, S, t);
+#pragma unroll 1
+  for (int b = ebits - 2; b >= 0; --b) {
+    mont_sqr<LC>(t, acol, S, n2, k.d.n2_minv);
+    if ((e[b >> 5] >> (b & 31)) & 1u) mont_mul<LC>(t, LdsCol{bcol, S}, n2, k.d.n2_minv);
+  }
+  redc<LC>(t, n2, k.d.n2_minv);
+  store_g<LC>(out + i * LC, t);
+}
+
+// ------------------------------------------------------------------------------------------
+// limbs <-> hex text (mpz_get_str(..., 16) / mpz_set_str(..., 16))
+// ------------------------------------------------------------------------------------------
+
+// number of characters of each element's hex text ('-' included), "0" for zero
+__global__ __launch_bounds__(256) void k_hex_len(const uint32_t* __restrict__ limbs, int L,
+                                                 const signed char* __restrict__ neg,
+                                                 long long* __restrict__ lens, long long N) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const uint32_t* x = limbs + i * L;
+  int digits = 1;
+  for (int w = L - 1; w >= 0; --w)
+    if (x[w]) { digits = w * 8 + (32 - __clz(x[w]) + 3) / 4; break; }
+  const bool zero = digits == 1 && x[0] == 0;
+  lens[i] = digits + ((neg && neg[i] && !zero) ? 1 : 0);
+}
+
+__global__ __launch_bounds__(256) void k_hex_write(const uint32_t* __restrict__ limbs, int L,
+                                                   const signed char* __restrict__ neg,
+                                                   const long long* __restrict__ offs,
+                                                   char* __restrict__ chars, long long N) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const uint32_t* x = limbs + i * L;
+  char* o = chars + offs[i];
+  long long len = offs[i + 1] - offs[i];
+  long long pos = 0;
+  int digits = (int)len;
+  if (len > 1 && neg && neg[i]) { o[pos++] = '-'; digits -= 1; }
+  for (int d = digits - 1; d >= 0; --d) {
+    const uint32_t v = (x[d >> 3] >> ((d & 7) * 4)) & 15u;
+    o[pos++] = (char)(v < 10 ? '0' + v : 'a' + v - 10);
+  }
+}
+
+// parse [-]hexdigits into L limbs; bad <- smallest index of a malformed / too-wide string
+__global__ __launch_bounds__(256) void k_hex_parse(const char* __restrict__ chars,
+                                                   const long long* __restrict__ offs, int L,
+                                                   uint32_t* __restrict__ limbs,
+                                                   signed char* __restrict__ neg, long long N,
+                                                   unsigned long long* bad) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  long long s = offs[i];
+  const long long e = offs[i + 1];
+  uint32_t* x = limbs + i * L;
+  for (int w = 0; w < L; ++w) x[w] = 0;
+  bool ok = e > s, ng = false;
+  if (ok && chars[s] == '-') { ng = true; ++s; ok = e > s; }
+  while (ok && s < e - 1 && chars[s] == '0') ++s;
+  if (ok && e - s > 8LL * L) ok = false;
+  for (long long j = e - 1, d = 0; ok && j >= s; --j, ++d) {
+    const char c = chars[j];
+    uint32_t v;
+    if (c >= '0' && c <= '9') v = c - '0';
+    else if (c >= 'a' && c <= 'f') v = c - 'a' + 10;
+    else if (c >= 'A' && c <= 'F') v = c - 'A' + 10;
+    else { ok = false; break; }
+    x[d >> 3] |= v << ((d & 7) * 4);
+  }
+  if (neg) neg[i] = ng ? 1 : 0;
+  if (!ok) atomicMin(bad, (unsigned long long)i);
+}
+
+// decrypt -> int64 (mpz_get_sll semantics, gmp_utils.cc:38-45: low 64 bits of |m|, then sign)
+__global__ __launch_bounds__(256) void k_to_int64(const uint32_t* __restrict__ mag, int L,
+                                                  const signed char* __restrict__ neg,
+                                                  long long* __restrict__ out, long long N) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const uint64_t v = (uint64_t)mag[i * L] | ((uint64_t)mag[i * L + 1] << 32);
+  out[i] = neg[i] ? (long long)(0ull - v) : (long long)v;
+}
+
+// ------------------------------------------------------------------------------------------
+// dispatch
+// ------------------------------------------------------------------------------------------
+
+inline bool key_ok(const efl_pl_key* d, bool need_private, int ln_max) {
+  if (!d) { set_error("null key descriptor"); return false; }
+  if (d->ln != 16 && d->ln != 32 && d->ln != 64 && d->ln != 128) {
+    set_error("unsupported limb count %d (n of 512/1024/2048/4096 bits)", d->ln);
+    return false;
+  }
+  if (d->ln > ln_max) {
+    set_error("n of %d bits is not supported by this operation on the GPU yet (max %d)", d->ln * 32, ln_max * 32);
+    return false;
+  }
+  if (need_private && !d->has_private) { set_error("No private key."); return false; }
+  return true;
+}
+
+inline unsigned grid_of(long long N) { return (unsigned)((N + kPlBlock - 1) / kPlBlock); }
+
+template <template <int> class F, class... A>
+hipError_t dispatch_ln(int ln, A... args) {
+  switch (ln) {
+    case 16: return F<16>::run(args...);
+    case 32: return F<32>::run(args...);
+    case 64: return F<64>::run(args...);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int LN>
+struct RunEncrypt {
+  static hipError_t run(Key k, const long long* m, const uint32_t* hsa, uint32_t* out, long long N,
+                        uint64_t seed, long long ctr0, hipStream_t s) {
+    const size_t lds = (size_t)2 * (2 * LN) * kPlBlock * 4;
+    hipLaunchKernelGGL((k_encrypt<LN>), dim3(grid_of(N)), dim3(kPlBlock), lds, s, k, m, hsa, out, N, seed, ctr0);
+    return hipGetLastError();
+  }
+};
+template <int LN>
+struct RunFbpowm {
+  static hipError_t run(Key k, const uint32_t* a, uint32_t* out, long long N, uint64_t seed, long long ctr0,
+                        hipStream_t s) {
+    const size_t lds = (size_t)2 * (2 * LN) * kPlBlock * 4;
+    hipLaunchKernelGGL((k_fbpowm<LN>), dim3(grid_of(N)), dim3(kPlBlock), lds, s, k, a, out, N, seed, ctr0);
+    return hipGetLastError();
+  }
+};
+template <int LN>
+struct RunAdd {
+  static hipError_t run(Key k, const uint32_t* x, const uint32_t* y, uint32_t* out, long long N, hipStream_t s) {
+    const size_t lds = (size_t)(2 * LN) * kPlBlock * 4;
+    hipLaunchKernelGGL((k_add<LN>), dim3(grid_of(N)), dim3(kPlBlock), lds, s, k, x, y, out, N);
+    return hipGetLastError();
+  }
+};
+template <int LN>
+struct RunPowm {
+  static hipError_t run(Key k, const uint32_t* x, const uint32_t* e, int ew, uint32_t* out, long long N,
+                        hipStream_t s) {
+    const size_t lds = (size_t)2 * (2 * LN) * kPlBlock * 4;
+    hipLaunchKernelGGL((k_powm<LN>), dim3(grid_of(N)), dim3(kPlBlock), lds, s, k, x, e, ew, out, N);
+    return hipGetLastError();
+  }
+};
+
+template <int LP>
+hipError_t run_decrypt(Key k, const uint32_t* ct, uint32_t* mag, signed char* neg, long long N, hipStream_t s) {
+  const size_t lds = (size_t)2 * LP * kPlBlock * 4;
+  hipLaunchKernelGGL((k_decrypt<LP>), dim3(grid_of(N)), dim3(kPlBlock), lds, s, k, ct, mag, neg, N);
+  return hipGetLastError();
+}
+
+}  // namespace
+}  // namespace efl
+
+using namespace efl;
+
+EFL_API int efl_pl_encrypt(const void* key_block, const efl_pl_key* key, const int64_t* plaintext,
+                           const uint32_t* hsa, uint32_t* ciphertext, int64_t n, uint64_t seed,
+                           int64_t counter_base, void* stream) {
+  if (!key_ok(key, false, 64)) return EFL_E_INVALID_ARGUMENT;
+  if (n < 0) { set_error("negative count"); return EFL_E_INVALID_ARGUMENT; }
+  if (n == 0) return EFL_OK;
+  if (!hsa && (key->table_rows <= 0 || key->group_size <= 0)) {
+    set_error("no fixed-base table: set the public key first");
+    return EFL_E_ABORTED;
+  }
+  Key k{(const uint32_t*)key_block, *key};
+  return hip_status(dispatch_ln<RunEncrypt>(key->ln, k, (const long long*)plaintext, hsa, ciphertext,
+                                             (long long)n, seed, (long long)counter_base, (hipStream_t)stream),
+                    "efl_pl_encrypt");
+}
+
+EFL_API int efl_pl_fbpowm(const void* key_block, const efl_pl_key* key, const uint32_t* a, uint32_t* hsa,
+                          int64_t n, uint64_t seed, int64_t counter_base, void* stream) {
+  if (!key_ok(key, false, 64)) return EFL_E_INVALID_ARGUMENT;
+  if (n <= 0) return n < 0 ? EFL_E_INVALID_ARGUMENT : EFL_OK;
+  Key k{(const uint32_t*)key_block, *key};
+  return hip_status(dispatch_ln<RunFbpowm>(key->ln, k, a, hsa, (long long)n, seed, (long long)counter_base,
+                                            (hipStream_t)stream),
+                    "efl_pl_fbpowm");
+}
+
+EFL_API int efl_pl_decrypt(const void* key_block, const efl_pl_key* key, const uint32_t* ciphertext,
+                           uint32_t* magnitude, int8_t* negative, int64_t n, void* stream) {
+  if (!key_ok(key, true, 128)) return key && !key->has_private ? EFL_E_ABORTED : EFL_E_INVALID_ARGUMENT;
+  if (n < 0) { set_error("negative count"); return EFL_E_INVALID_ARGUMENT; }
+  if (n == 0) return EFL_OK;
+  Key k{(const uint32_t*)key_block, *key};
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e;
+  switch (key->ln) {
+    case 16: e = run_decrypt<16>(k, ciphertext, magnitude, (signed char*)negative, n, s); break;
+    case 32: e = run_decrypt<32>(k, ciphertext, magnitude, (signed char*)negative, n, s); break;
+    case 64: e = run_decrypt<64>(k, ciphertext, magnitude, (signed char*)negative, n, s); break;
+    default: e = run_decrypt<128>(k, ciphertext, magnitude, (signed char*)negative, n, s); break;
+  }
+  return hip_status(e, "efl_pl_decrypt");
+}
+
+EFL_API int efl_pl_add(const void* key_block, const efl_pl_key* key, const uint32_t* x, const uint32_t* y,
+                       uint32_t* z, int64_t n, void* stream) {
+  if (!key_ok(key, false, 64)) return EFL_E_INVALID_ARGUMENT;
+  if (n <= 0) return n < 0 ? EFL_E_INVALID_ARGUMENT : EFL_OK;
+  Key k{(const uint32_t*)key_block, *key};
+  return hip_status(dispatch_ln<RunAdd>(key->ln, k, x, y, z, (long long)n, (hipStream_t)stream), "efl_pl_add");
+}
+
+EFL_API int efl_pl_powm(const void* key_block, const efl_pl_key* key, const uint32_t* x, const uint32_t* exps,
+                        int exp_words, uint32_t* z, int64_t n, void* stream) {
+  if (!key_ok(key, false, 64)) return EFL_E_INVALID_ARGUMENT;
+  if (exp_words <= 0) { set_error("exp_words must be positive"); return EFL_E_INVALID_ARGUMENT; }
+  if (n <= 0) return n < 0 ? EFL_E_INVALID_ARGUMENT : EFL_OK;
+  Key k{(const uint32_t*)key_block, *key};
+  return hip_status(dispatch_ln<RunPowm>(key->ln, k, x, exps, exp_words, z, (long long)n, (hipStream_t)stream),
+                    "efl_pl_powm");
+}
+
+EFL_API int efl_hex_lengths(const uint32_t* limbs, int limbs_per_elem, const int8_t* negative,
+                            int64_t* lengths, int64_t n, void* stream) {
+  if (n <= 0) return n < 0 ? EFL_E_INVALID_ARGUMENT : EFL_OK;
+  hipLaunchKernelGGL(k_hex_len, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, limbs,
+                     limbs_per_elem, (const signed char*)negative, (long long*)lengths, (long long)n);
+  return hip_status(hipGetLastError(), "efl_hex_lengths");
+}
+
+EFL_API int efl_hex_write(const uint32_t* limbs, int limbs_per_elem, const int8_t* negative,
+                          const int64_t* offsets, char* chars, int64_t n, void* stream) {
+  if (n <= 0) return n < 0 ? EFL_E_INVALID_ARGUMENT : EFL_OK;
+  hipLaunchKernelGGL(k_hex_write, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, limbs,
+                     limbs_per_elem, (const signed char*)negative, (const long long*)offsets, chars, (long long)n);
+  return hip_status(hipGetLastError(), "efl_hex_write");
+}
+
+EFL_API int efl_hex_parse(const char* chars, const int64_t* offsets, int limbs_per_elem, uint32_t* limbs,
+                          int8_t* negative, int64_t n, int64_t* bad, void* stream) {
+  if (!bad) { set_error("null status word"); return EFL_E_INVALID_ARGUMENT; }
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = hipMemsetAsync(bad, 0xFF, sizeof(int64_t), s);
+  if (e != hipSuccess || n <= 0) return hip_status(e, "efl_hex_parse");
+  hipLaunchKernelGGL(k_hex_parse, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, chars,
+                     (const long long*)offsets, limbs_per_elem, limbs, (signed char*)negative, (long long)n,
+                     (unsigned long long*)bad);
+  return hip_status(hipGetLastError(), "efl_hex_parse");
+}
+
+EFL_API int efl_pl_to_int64(const uint32_t* magnitude, int limbs_per_elem, const int8_t* negative,
+                            int64_t* out, int64_t n, void* stream) {
+  if (n <= 0) return n < 0 ? EFL_E_INVALID_ARGUMENT : EFL_OK;
+  if (limbs_per_elem < 2) { set_error("need >= 2 limbs"); return EFL_E_INVALID_ARGUMENT; }
+  hipLaunchKernelGGL(k_to_int64, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     magnitude, limbs_per_elem, (const signed char*)negative, (long long*)out, (long long)n);
+  return hip_status(hipGetLastError(), "efl_pl_to_int64");
+}

@@ -3,9 +3,10 @@
 In efls-train, Paillier ciphertexts and decrypted big plaintexts travel as `tf.string` tensors
 whose elements are lowercase hex numbers written by `mpz_get_str(..., 16)`
 (efls-train/cc/efl/math/gmp_utils.cc:146-150, paillier.cc:127,140). A HexTensor holds the same
-strings packed back to back (one flat uint8 buffer + int64 offsets[n+1], i.e. a ragged array) with
-a shape, so they can be moved to HBM in two copies and parsed by kernels, and it serialises to
-TensorProto.tensor_content exactly like TF's string encoding (varint lengths, then bytes).
+strings packed back to back (one flat byte buffer + int64 offsets[n+1], a ragged array) with a
+shape. It can live on the host (numpy) or in HBM (torch device tensors, as produced by the hex
+kernels); each side is materialised on first use. It serialises to TensorProto.tensor_content
+exactly like TF's string encoding (all varint32 lengths, then the bytes).
 """
 from __future__ import annotations
 
@@ -14,14 +15,15 @@ import torch
 
 
 class HexTensor:
-    __slots__ = ("buf", "offs", "shape", "_dev_cache")
+    __slots__ = ("_buf", "_offs", "shape", "_dev")
 
-    def __init__(self, buf: np.ndarray, offs: np.ndarray, shape):
-        self.buf = np.ascontiguousarray(buf, np.uint8)
-        self.offs = np.ascontiguousarray(offs, np.int64)
+    def __init__(self, buf: np.ndarray | None, offs: np.ndarray | None, shape, device_parts=None):
+        self._buf = None if buf is None else np.ascontiguousarray(buf, np.uint8)
+        self._offs = None if offs is None else np.ascontiguousarray(offs, np.int64)
         self.shape = tuple(int(s) for s in shape)
-        self._dev_cache = None
-        if int(np.prod(self.shape, dtype=np.int64)) != self.offs.size - 1:
+        self._dev = device_parts          # (device, chars uint8 tensor, offsets int64 tensor)
+        n = self._offs.size - 1 if self._offs is not None else int(device_parts[2].numel()) - 1
+        if int(np.prod(self.shape, dtype=np.int64)) != n:
             raise ValueError("HexTensor: shape does not match the number of strings")
 
     # -- construction ---------------------------------------------------------------------
@@ -45,13 +47,42 @@ class HexTensor:
         strs = [("-" + format(-v, "x")) if v < 0 else format(v, "x") for v in vals]
         return cls.from_strings(np.array(strs, dtype=object).reshape(shape if shape is not None else (len(strs),)))
 
-    # -- access ---------------------------------------------------------------------------
-    def numel(self) -> int:
-        return self.offs.size - 1
+    @classmethod
+    def from_device(cls, chars: torch.Tensor, offs: torch.Tensor, shape):
+        return cls(None, None, shape, (chars.device, chars, offs))
 
+    # -- storage --------------------------------------------------------------------------
+    @property
+    def buf(self) -> np.ndarray:
+        if self._buf is None:
+            _, chars, offs = self._dev
+            total = int(offs[-1].item()) if offs.numel() else 0
+            self._buf = chars[:total].cpu().numpy() if total else np.zeros(0, np.uint8)
+        return self._buf
+
+    @property
+    def offs(self) -> np.ndarray:
+        if self._offs is None:
+            self._offs = self._dev[2].cpu().numpy()
+        return self._offs
+
+    def numel(self) -> int:
+        return (self._offs.size if self._offs is not None else int(self._dev[2].numel())) - 1
+
+    def device_buffers(self, device):
+        """(chars uint8, offsets int64) on `device` (copied once, cached)."""
+        if self._dev is None or self._dev[0] != device:
+            host = self.buf if self.buf.size else np.zeros(1, np.uint8)
+            chars = torch.from_numpy(np.array(host, copy=True)).to(device)
+            offs = torch.from_numpy(np.array(self.offs, copy=True)).to(device)
+            self._dev = (device, chars, offs)
+        return self._dev[1], self._dev[2]
+
+    # -- access ---------------------------------------------------------------------------
     def strings(self):
         b = self.buf.tobytes()
-        return [b[self.offs[i]:self.offs[i + 1]].decode() for i in range(self.numel())]
+        o = self.offs
+        return [b[o[i]:o[i + 1]].decode() for i in range(self.numel())]
 
     def to_ints(self):
         return [int(s, 16) for s in self.strings()]
@@ -59,9 +90,10 @@ class HexTensor:
     def numpy(self) -> np.ndarray:
         """object ndarray of bytes, the way a TF string tensor reads back in Python."""
         b = self.buf.tobytes()
+        o = self.offs
         out = np.empty(self.numel(), dtype=object)
         for i in range(self.numel()):
-            out[i] = b[self.offs[i]:self.offs[i + 1]]
+            out[i] = b[o[i]:o[i + 1]]
         return out.reshape(self.shape)
 
     def reshape(self, shape):
@@ -69,7 +101,7 @@ class HexTensor:
         if -1 in shape:
             known = int(np.prod([s for s in shape if s != -1], dtype=np.int64)) or 1
             shape = tuple(self.numel() // known if s == -1 else s for s in shape)
-        return HexTensor(self.buf, self.offs, shape)
+        return HexTensor(self._buf, self._offs, shape, self._dev)
 
     def transpose(self):
         if len(self.shape) != 2:
@@ -80,29 +112,20 @@ class HexTensor:
 
     def take(self, idx, shape):
         idx = np.asarray(idx, np.int64).reshape(-1)
-        lens = self.offs[1:] - self.offs[:-1]
+        offs0, buf0 = self.offs, self.buf
+        lens = offs0[1:] - offs0[:-1]
         nl = lens[idx]
         offs = np.zeros(idx.size + 1, np.int64)
         offs[1:] = np.cumsum(nl)
-        starts = self.offs[idx]
+        starts = offs0[idx]
         if offs[-1]:
             gather = np.repeat(starts - offs[:-1], nl) + np.arange(offs[-1])
-            buf = self.buf[gather]
+            buf = buf0[gather]
         else:
             buf = np.zeros(0, np.uint8)
         return HexTensor(buf, offs, shape)
 
-    def device_buffers(self, device):
-        """(chars uint8, offsets int64) on `device`, cached."""
-        if self._dev_cache is None or self._dev_cache[0] != device:
-            host = self.buf if self.buf.size else np.zeros(1, np.uint8)
-            chars = torch.from_numpy(np.array(host, copy=not host.flags.writeable)).to(device)
-            offs = torch.from_numpy(self.offs).to(device)
-            self._dev_cache = (device, chars, offs)
-        return self._dev_cache[1], self._dev_cache[2]
-
-    # -- TF DT_STRING tensor_content codec (tensorflow/core/platform/tensor_coding.cc
-    #    EncodeStringList: all varint32 lengths, then all bytes) --------------------------------
+    # -- TF DT_STRING tensor_content codec (EncodeStringList: varint32 lengths, then bytes) ----
     def to_tensor_content(self) -> bytes:
         lens = (self.offs[1:] - self.offs[:-1]).tolist()
         out = bytearray()

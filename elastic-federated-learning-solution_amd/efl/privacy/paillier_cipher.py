@@ -1,0 +1,601 @@
+"""Paillier keypair, ciphertext tensors and homomorphic ops on the MI355X (Stage P).
+
+Drop-in for efls-train/python/efl/privacy/paillier.py:29-205 (`efl.paillier.Keypair`,
+`efl.paillier.Tensor`, FixedPointTensor arithmetic). The per-element arithmetic runs in
+libefl_hip.so (csrc/paillier.hip); this module does what the reference's PaillierKeypair resource
+does on the host once per key (paillier.cc:50-101, SetPublicKey / SetPrivateKey, the fbpowm table
+of gmp_utils.cc:56-89): derive the key constants with exact integer arithmetic, add the Montgomery
+constants the kernels need, and upload everything as one device "key block" (include/efl_hip.h,
+efl_pl_key).
+
+Ciphertexts stay in HBM as fixed-width limb rows (CipherTensor, [N, 2*ln] uint32); hex text (the
+reference's DT_STRING) is produced or parsed on the GPU only when a tensor crosses the wire or is
+handed to string-typed callers.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+import secrets
+
+import numpy as np
+import torch
+
+from efl import errors, exporter
+from efl import lib as _efl_lib
+from efl.privacy.hex_tensor import HexTensor
+
+_lib = _efl_lib.raw()
+_vp, _i64, _i32, _u64 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_uint64
+
+
+class PlKey(ctypes.Structure):
+    """ctypes mirror of efl_pl_key (include/efl_hip.h)."""
+    _fields_ = [(n, ctypes.c_int32) for n in ("ln", "a_bits", "group_size", "table_rows", "table_cols",
+                                               "has_private", "pm1_bits", "qm1_bits")] + \
+               [(n, ctypes.c_uint32) for n in ("n2_minv", "p2_minv", "q2_minv", "p_minv", "q_minv")] + \
+               [(n, ctypes.c_int64) for n in ("off_n", "off_n2", "off_n2_r2", "off_n2_one", "off_table", "off_max",
+                                               "off_p", "off_q", "off_p2", "off_q2", "off_p2_r3", "off_q2_r3",
+                                               "off_pm1", "off_qm1", "off_pinv_w", "off_qinv_w", "off_hp",
+                                               "off_hq", "off_qinvp")]
+
+
+_PK = ctypes.POINTER(PlKey)
+for _name, _args in {
+    "efl_pl_encrypt": [_vp, _PK, _vp, _vp, _vp, _i64, _u64, _i64, _vp],
+    "efl_pl_fbpowm": [_vp, _PK, _vp, _vp, _i64, _u64, _i64, _vp],
+    "efl_pl_decrypt": [_vp, _PK, _vp, _vp, _vp, _i64, _vp],
+    "efl_pl_add": [_vp, _PK, _vp, _vp, _vp, _i64, _vp],
+    "efl_pl_powm": [_vp, _PK, _vp, _vp, _i32, _vp, _i64, _vp],
+    "efl_hex_lengths": [_vp, _i32, _vp, _vp, _i64, _vp],
+    "efl_hex_write": [_vp, _i32, _vp, _vp, _vp, _i64, _vp],
+    "efl_hex_parse": [_vp, _vp, _i32, _vp, _vp, _i64, _vp, _vp],
+    "efl_pl_to_int64": [_vp, _i32, _vp, _vp, _i64, _vp],
+}.items():
+    getattr(_lib, _name).argtypes = _args
+    getattr(_lib, _name).restype = _i32
+
+_LIMB_CLASSES = (16, 32, 64, 128)
+MAX_TABLE_BITS = 1 << 40      # gmp_utils.h:20 FBPOWM_MAX_TABLE_MEM, compared against entries x bits
+
+
+def _limbs(x: int, L: int) -> np.ndarray:
+    return np.frombuffer(int(x).to_bytes(4 * L, "little"), dtype="<u4").copy()
+
+
+def _minv32(m: int) -> int:
+    return (-pow(m, -1, 1 << 32)) % (1 << 32)
+
+
+def _hex_of(v) -> str:
+    """Scalar hex text from str/bytes/HexTensor/0-d tensor/np array element."""
+    if isinstance(v, HexTensor):
+        v = v.strings()[0]
+    elif isinstance(v, np.ndarray):
+        v = v.reshape(-1)[0]
+    elif isinstance(v, (list, tuple)):
+        v = v[0]
+    if isinstance(v, (bytes, bytearray)):
+        v = v.decode()
+    return str(v)
+
+
+def _int_of(v) -> int:
+    if isinstance(v, torch.Tensor):
+        return int(v.reshape(-1)[0].item())
+    if isinstance(v, (np.ndarray, list, tuple)):
+        return int(np.asarray(v).reshape(-1)[0])
+    return int(v)
+
+
+# ----------------------------------------------------------------------------------------------
+# key generation (GeneratePaillierKeypairOp, paillier.cc:833-904), host side, once per session
+# ----------------------------------------------------------------------------------------------
+
+_SMALL_PRIMES = [p for p in range(3, 2000) if all(p % d for d in range(2, int(p ** 0.5) + 1))]
+
+
+def _probable_prime(x: int, reps: int, rng) -> bool:
+    if x < 2:
+        return False
+    for p in _SMALL_PRIMES:
+        if x % p == 0:
+            return x == p
+    d, s = x - 1, 0
+    while d % 2 == 0:
+        d //= 2
+        s += 1
+    for _ in range(reps):
+        a = 2 + rng.randbelow(x - 3)
+        y = pow(a, d, x)
+        if y in (1, x - 1):
+            continue
+        for _ in range(s - 1):
+            y = y * y % x
+            if y == x - 1:
+                break
+        else:
+            return False
+    return True
+
+
+def generate_keypair_ints(n_bytes=512, reps=24, rng=None):
+    """(n, hs, p, q) with the reference's construction: primes of n_bytes*4 bits with bits 0, 1
+    and the top bit set, gcd(p-1, q-1) = 2, hs = (-x^2)^n mod n^2 for a random x in Z_n^*."""
+    rng = rng or secrets.SystemRandom()
+    bits = n_bytes * 4
+
+    def draw():
+        while True:
+            c = rng.getrandbits(bits) | 3 | (1 << (bits - 1))
+            if _probable_prime(c, reps, rng):
+                return c
+    while True:
+        p, q = draw(), draw()
+        if math.gcd(p - 1, q - 1) == 2 and p != q:
+            break
+    n = p * q
+    while True:
+        x = rng.randrange(1, n)
+        if math.gcd(x, n) == 1:
+            break
+    hs = pow((-x * x) % n, n, n * n)
+    return n, hs, p, q
+
+
+# ----------------------------------------------------------------------------------------------
+# device key block
+# ----------------------------------------------------------------------------------------------
+
+class KeyBlock:
+    """Host derivation + device upload of every constant the kernels read (efl_pl_key)."""
+
+    def __init__(self, n: int, hs: int, a_bits: int, group_size: int, p=None, q=None, device=None):
+        if n.bit_length() < 128:
+            raise errors.UnimplementedError("n of fewer than 128 bits is not supported on the GPU")
+        if p is not None and q is not None and q >= 2 * p:
+            p, q = q, p        # CRT below reduces mq mod p with one subtraction: needs q < 2p
+        self.n, self.hs, self.p, self.q = n, hs, p, q
+        self.a_bits, self.group_size = a_bits, group_size
+        need = max(n.bit_length(), 2 * max(p or 0, q or 0).bit_length())
+        ln = next((c for c in _LIMB_CLASSES if 32 * c >= need), None)
+        if ln is None:
+            raise errors.UnimplementedError(f"n of {n.bit_length()} bits: at most 4096 supported")
+        self.ln, self.lc, self.lh = ln, 2 * ln, ln // 2
+        self.device = device or _efl_lib.require_gpu()
+        self.desc = PlKey()
+        words = []
+        pos = [0]
+
+        def put(x: int, L: int) -> int:
+            off = pos[0]
+            words.append(_limbs(x, L))
+            pos[0] += L
+            return off
+
+        d = self.desc
+        n2 = n * n
+        Rc = 1 << (32 * self.lc)
+        d.ln, d.a_bits, d.group_size = ln, a_bits, group_size
+        d.off_n = put(n, ln)
+        d.off_n2 = put(n2, self.lc)
+        d.off_n2_r2 = put(Rc * Rc % n2, self.lc)
+        d.off_n2_one = put(Rc % n2, self.lc)
+        d.off_max = put(-(-(2 * n) // 3), ln)
+        d.n2_minv = _minv32(n2)
+        if p is not None and q is not None:
+            Rp, Rh = 1 << (32 * ln), 1 << (32 * self.lh)
+            d.has_private = 1
+            d.off_p, d.off_q = put(p, self.lh), put(q, self.lh)
+            d.off_p2, d.off_q2 = put(p * p, ln), put(q * q, ln)
+            d.p2_minv, d.q2_minv = _minv32(p * p), _minv32(q * q)
+            d.p_minv, d.q_minv = _minv32(p), _minv32(q)
+            d.off_p2_r3 = put(pow(Rp, 3, p * p), ln)
+            d.off_q2_r3 = put(pow(Rp, 3, q * q), ln)
+            d.off_pm1, d.off_qm1 = put(p - 1, self.lh), put(q - 1, self.lh)
+            d.pm1_bits, d.qm1_bits = (p - 1).bit_length(), (q - 1).bit_length()
+            d.off_pinv_w = put(pow(p, -1, Rh), self.lh)
+            d.off_qinv_w = put(pow(q, -1, Rh), self.lh)
+            hp = pow((pow(n + 1, p - 1, p * p) - 1) // p, -1, p)      # paillier.cc:28-37
+            hq = pow((pow(n + 1, q - 1, q * q) - 1) // q, -1, q)
+            d.off_hp = put(hp * Rh % p, self.lh)
+            d.off_hq = put(hq * Rh % q, self.lh)
+            d.off_qinvp = put(pow(q, -1, p) * Rh % p, self.lh)
+        # fixed-base table T[i][j] = hs^((j+1) 2^(g i)) mod n^2, Montgomery form (gmp_utils.cc:56-89)
+        g = group_size
+        cols = (1 << g) - 1
+        rows = a_bits // g + (1 if a_bits % g else 0)
+        if rows * cols * n2.bit_length() > MAX_TABLE_BITS:
+            raise errors.ResourceExhaustedError("Memory usage exceeds a predefined threshold.")
+        d.table_rows, d.table_cols = rows, cols
+        d.off_table = pos[0]
+        entry = hs % n2
+        row = []
+        acc = entry
+        for j in range(cols):                 # row 0: hs^1 .. hs^cols
+            row.append(acc)
+            acc = acc * entry % n2
+        tab = np.empty((rows, cols, self.lc), dtype="<u4")
+        nbytes = 4 * self.lc
+        for i in range(rows):
+            if i:
+                sq = 1 << g
+                row = [pow(v, sq, n2) for v in row]
+            buf = b"".join((v * Rc % n2).to_bytes(nbytes, "little") for v in row)
+            tab[i] = np.frombuffer(buf, dtype="<u4").reshape(cols, self.lc)
+        words.append(tab.reshape(-1))
+        pos[0] += tab.size
+        host = np.concatenate(words)
+        self.block = torch.from_numpy(host.view(np.int32)).to(self.device)
+        self.ptr = self.block.data_ptr()
+
+    def args(self):
+        return self.ptr, ctypes.byref(self.desc)
+
+
+# ----------------------------------------------------------------------------------------------
+# ciphertext tensors
+# ----------------------------------------------------------------------------------------------
+
+def _stream(dev):
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def limbs_to_hex(limbs: torch.Tensor, neg: torch.Tensor | None, shape) -> HexTensor:
+    """[N, L] uint32 limbs (+ optional sign bytes) -> device HexTensor (mpz_get_str(..., 16))."""
+    N, L = limbs.shape[0], limbs.shape[1]
+    dev = limbs.device
+    lens = torch.empty(N, dtype=torch.int64, device=dev)
+    negp = neg.data_ptr() if neg is not None else None
+    _efl_lib.check(_lib.efl_hex_lengths(limbs.data_ptr(), L, negp, lens.data_ptr(), N, _stream(dev)))
+    offs = torch.zeros(N + 1, dtype=torch.int64, device=dev)
+    if N:
+        torch.cumsum(lens, 0, out=offs[1:])
+    total = int(offs[-1].item()) if N else 0
+    chars = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
+    _efl_lib.check(_lib.efl_hex_write(limbs.data_ptr(), L, negp, offs.data_ptr(), chars.data_ptr(), N,
+                                      _stream(dev)))
+    return HexTensor.from_device(chars, offs, shape)
+
+
+def hex_to_limbs(hx: HexTensor, L: int, device, signed=False):
+    """HexTensor -> ([N, L] limbs, sign bytes or None); InvalidArgument on malformed/too wide text."""
+    N = hx.numel()
+    chars, offs = hx.device_buffers(device)
+    limbs = torch.empty((N, L), dtype=torch.int32, device=device)
+    neg = torch.empty(N, dtype=torch.int8, device=device) if signed else None
+    bad = torch.empty(1, dtype=torch.int64, device=device)
+    _efl_lib.check(_lib.efl_hex_parse(chars.data_ptr(), offs.data_ptr(), L, limbs.data_ptr(),
+                                      neg.data_ptr() if neg is not None else None, N, bad.data_ptr(),
+                                      _stream(device)))
+    b = int(bad.item())
+    if b >= 0:
+        raise errors.InvalidArgumentError(f"element {b} is not a hex integer of at most {32 * L} bits: "
+                                          f"{hx.strings()[b][:40]!r}")
+    return limbs, neg
+
+
+class CipherTensor:
+    """Paillier ciphertexts in HBM: limbs [N, 2*ln] (int32 storage of uint32 limbs) + shape."""
+
+    def __init__(self, limbs: torch.Tensor, shape, key: KeyBlock):
+        self.limbs, self.shape, self.key = limbs, tuple(int(s) for s in shape), key
+
+    def numel(self):
+        return self.limbs.shape[0]
+
+    def to_hex(self) -> HexTensor:
+        return limbs_to_hex(self.limbs, None, self.shape)
+
+    def reshape(self, shape):
+        shape = tuple(int(s) for s in shape)
+        if -1 in shape:
+            known = int(np.prod([s for s in shape if s != -1])) or 1
+            shape = tuple(self.numel() // known if s == -1 else s for s in shape)
+        return CipherTensor(self.limbs, shape, self.key)
+
+    def transpose(self):
+        r, c = self.shape
+        idx = torch.arange(r * c, device=self.limbs.device).reshape(r, c).t().reshape(-1)
+        return CipherTensor(self.limbs[idx].contiguous(), (c, r), self.key)
+
+    def __repr__(self):
+        return f"CipherTensor(shape={self.shape}, {32 * self.limbs.shape[1]}-bit)"
+
+
+# ----------------------------------------------------------------------------------------------
+# public API (efl.paillier.*)
+# ----------------------------------------------------------------------------------------------
+
+@exporter.export("paillier.Tensor")
+class PaillierTensor(object):
+    """paillier.py:29-50."""
+
+    def __init__(self, keypair, tensor):
+        self.keypair = keypair
+        self.tensor = tensor
+
+    def __add__(self, another):
+        if not isinstance(another, PaillierTensor):
+            another = self.keypair.encrypt(another)
+        return PaillierTensor(self.keypair, self.keypair.add(self.tensor, another.tensor))
+
+    def __mul__(self, scalar):
+        return PaillierTensor(self.keypair, self.keypair.mul_scalar(self.tensor, scalar))
+
+    def decrypt(self, dtype="string"):
+        return self.keypair.decrypt(self, dtype)
+
+    def __lshift__(self, exp):
+        return PaillierTensor(self.keypair, self.keypair.mul_exp2(self.tensor, exp))
+
+    @property
+    def shape(self):
+        return self.tensor.shape
+
+
+def _is_string_dtype(dtype) -> bool:
+    return dtype in ("string", str, bytes, "str") or getattr(dtype, "name", None) == "string"
+
+
+@exporter.export("paillier.Keypair")
+class PaillierKeypair(object):
+    """paillier.py:53-104 over the PaillierKeypair resource (paillier.cc:50-331)."""
+
+    def __init__(self, seed: bytes | int | None = None):
+        self._key: KeyBlock | None = None
+        self._n_bytes = None
+        if seed is None:
+            seed = os.urandom(8)
+        if isinstance(seed, (bytes, bytearray)):
+            seed = int.from_bytes(bytes(seed)[:8].ljust(8, b"\0"), "little")
+        self.seed = int(seed) & ((1 << 64) - 1)
+        self.counter = 0
+
+    # -- key management ------------------------------------------------------------------
+    def initialize(self):
+        """CreatePaillierKeypair: the resource exists from construction; kept for the API."""
+        return None
+
+    def generate_keypair(self, n_bytes=None, reps=None, a_bytes=None, group_size=None, rng=None):
+        """GeneratePaillierKeypair (attr defaults n_bytes=512, a_bytes=256, reps=24, group_size=1).
+        Returns (public_key [n, hs], private_key [p, q]) as HexTensors."""
+        n_bytes = 512 if n_bytes is None else int(n_bytes)
+        a_bytes = 256 if a_bytes is None else int(a_bytes)
+        reps = 24 if reps is None else int(reps)
+        group_size = 1 if group_size is None else int(group_size)
+        n, hs, p, q = generate_keypair_ints(n_bytes, reps, rng)
+        self._set(n, n_bytes, hs, a_bytes, group_size, p, q)
+        return HexTensor.from_ints([n, hs]), HexTensor.from_ints([p, q])
+
+    def set_public_key(self, n, n_bytes, hs, a_bytes, group_size=None):
+        """SetPaillierPublicKey. As in paillier.py:69-70 the group_size argument is not forwarded:
+        the table is built with the op's default group size 1."""
+        self._set(int(_hex_of(n), 16), _int_of(n_bytes), int(_hex_of(hs), 16), _int_of(a_bytes), 1)
+
+    def set_private_key(self, p, q):
+        """SetPaillierPrivateKey (ignored without a public key, paillier.cc:88-91)."""
+        if self._key is None:
+            return
+        k = self._key
+        self._set(k.n, self._n_bytes, k.hs, k.a_bits // 8, k.group_size,
+                  int(_hex_of(p), 16), int(_hex_of(q), 16))
+
+    def set_keys_ints(self, n, hs, a_bytes, group_size=1, p=None, q=None, n_bytes=None):
+        """Host-int variant of set_public_key/set_private_key (tests, key exchange)."""
+        self._set(n, n_bytes or (n.bit_length() + 7) // 8, hs, a_bytes, group_size, p, q)
+
+    def _set(self, n, n_bytes, hs, a_bytes, group_size, p=None, q=None):
+        self._key = KeyBlock(n, hs, 8 * int(a_bytes), int(group_size), p, q)
+        self._n_bytes = n_bytes
+
+    @property
+    def key(self) -> KeyBlock:
+        if self._key is None:
+            raise errors.AbortedError("No public key.")
+        return self._key
+
+    @property
+    def public_key(self):
+        return self.key.n, self.key.hs
+
+    # -- conversions ---------------------------------------------------------------------
+    def _cipher(self, x) -> CipherTensor:
+        """PaillierTensor / CipherTensor / HexTensor / strings -> CipherTensor of this key."""
+        if isinstance(x, PaillierTensor):
+            x = x.tensor
+        if isinstance(x, CipherTensor):
+            return x
+        k = self.key
+        hx = x if isinstance(x, HexTensor) else HexTensor.from_strings(x)
+        limbs, _ = hex_to_limbs(hx, k.lc, k.device)
+        return CipherTensor(limbs, hx.shape, k)
+
+    # -- ops -----------------------------------------------------------------------------
+    def encrypt(self, plaintext, hsa=None, counter_base=None):
+        """PaillierEncrypt (paillier.cc:443-503). hsa None (or all "0") draws a fresh a per element
+        from Philox(seed, counter); counter_base defaults to a running per-keypair counter."""
+        k = self.key
+        m = _efl_lib.as_tensor(plaintext)
+        if m.dtype != torch.int64:
+            m = m.to(torch.int64)
+        shape = tuple(m.shape)
+        m = m.reshape(-1).contiguous().to(k.device)
+        N = m.numel()
+        out = torch.empty((N, k.lc), dtype=torch.int32, device=k.device)
+        hsa_limbs = None
+        if hsa is not None:
+            hx = hsa if isinstance(hsa, HexTensor) else HexTensor.from_strings(hsa)
+            if hx.numel() != N:
+                raise errors.InvalidArgumentError("plaintext and hsa should be the same size.")
+            strs_zero = np.array([s in ("0", "-0", "") for s in hx.strings()]) if N else np.zeros(0, bool)
+            if not strs_zero.all():
+                hsa_limbs, _ = hex_to_limbs(hx, k.lc, k.device)
+            zero_idx = np.nonzero(strs_zero)[0] if hsa_limbs is not None else None
+        ctr = self.counter if counter_base is None else int(counter_base)
+        if counter_base is None:
+            self.counter += N
+        _efl_lib.check(_lib.efl_pl_encrypt(*k.args(), m.data_ptr(),
+                                           hsa_limbs.data_ptr() if hsa_limbs is not None else None,
+                                           out.data_ptr(), N, self.seed, ctr, _stream(k.device)))
+        if hsa_limbs is not None and zero_idx is not None and zero_idx.size:
+            idx = torch.from_numpy(zero_idx).to(k.device)
+            sub = torch.empty((idx.numel(), k.lc), dtype=torch.int32, device=k.device)
+            msub = m[idx].contiguous()
+            _efl_lib.check(_lib.efl_pl_encrypt(*k.args(), msub.data_ptr(), None, sub.data_ptr(), idx.numel(),
+                                               self.seed, ctr + N, _stream(k.device)))
+            out[idx] = sub
+        return PaillierTensor(self, CipherTensor(out, shape, k))
+
+    def fbpowm(self, a=None, n=None, counter_base=0):
+        """hs^(a') mod n^2 for given exponents (Python ints) or the Philox draw (FixedBasePowm)."""
+        k = self.key
+        words = (k.a_bits + 31) // 32
+        if a is not None:
+            a = list(a)
+            n = len(a)
+            arr = np.stack([_limbs(v, words) for v in a]) if n else np.zeros((0, words), "<u4")
+            a_dev = torch.from_numpy(arr.view(np.int32)).to(k.device)
+        out = torch.empty((n, k.lc), dtype=torch.int32, device=k.device)
+        _efl_lib.check(_lib.efl_pl_fbpowm(*k.args(), a_dev.data_ptr() if a is not None else None,
+                                          out.data_ptr(), n, self.seed, counter_base, _stream(k.device)))
+        return CipherTensor(out, (n,), k)
+
+    def decrypt(self, paillier_tensor, dtype="string"):
+        """PaillierDecrypt (paillier.cc:505-561): HexTensor of the signed plaintext (default) or
+        int64 (mpz_get_sll semantics)."""
+        k = self.key
+        if not k.desc.has_private:
+            raise errors.AbortedError("No private key.")
+        c = self._cipher(paillier_tensor)
+        N = c.numel()
+        mag = torch.empty((N, k.ln), dtype=torch.int32, device=k.device)
+        neg = torch.empty(N, dtype=torch.int8, device=k.device)
+        _efl_lib.check(_lib.efl_pl_decrypt(*k.args(), c.limbs.data_ptr(), mag.data_ptr(), neg.data_ptr(), N,
+                                           _stream(k.device)))
+        if _is_string_dtype(dtype):
+            return limbs_to_hex(mag, neg, c.shape)
+        if _efl_lib.to_torch_dtype(dtype) != torch.int64:
+            raise errors.InvalidArgumentError("PaillierDecrypt: dtype must be string or int64")
+        out = torch.empty(N, dtype=torch.int64, device=k.device)
+        _efl_lib.check(_lib.efl_pl_to_int64(mag.data_ptr(), k.ln, neg.data_ptr(), out.data_ptr(), N,
+                                            _stream(k.device)))
+        return out.reshape(c.shape)
+
+    def add(self, x, y):
+        """PaillierAdd: z = x * y mod n^2 (paillier.py:75-79 broadcasts first)."""
+        k = self.key
+        x, y = self._cipher(x), self._cipher(y)
+        x, y = _broadcast_pair(x, y)
+        out = torch.empty_like(x.limbs)
+        _efl_lib.check(_lib.efl_pl_add(*k.args(), x.limbs.data_ptr(), y.limbs.data_ptr(), out.data_ptr(),
+                                       x.numel(), _stream(k.device)))
+        return CipherTensor(out, x.shape, k)
+
+    def _powm(self, x: CipherTensor, exps: list[int]) -> CipherTensor:
+        k = self.key
+        N = x.numel()
+        emax = max((e.bit_length() for e in exps), default=1)
+        ew = max(1, (emax + 31) // 32)
+        arr = np.stack([_limbs(e, ew) for e in exps]) if N else np.zeros((0, ew), "<u4")
+        e_dev = torch.from_numpy(arr.view(np.int32)).to(k.device)
+        out = torch.empty_like(x.limbs)
+        _efl_lib.check(_lib.efl_pl_powm(*k.args(), x.limbs.data_ptr(), e_dev.data_ptr(), ew, out.data_ptr(), N,
+                                        _stream(k.device)))
+        return CipherTensor(out, x.shape, k)
+
+    def mul_scalar(self, x, scalar):
+        """PaillierMulScalar: x^y mod n^2 (negative y through the inverse, paillier.cc:180-265)."""
+        x = self._cipher(x)
+        ys = _scalar_list(scalar, x.shape)
+        x, ys = _broadcast_scalar(x, ys)
+        if any(y < 0 for y in ys):
+            raise errors.UnimplementedError("negative scalars need the ciphertext inverse (not yet on GPU)")
+        return self._powm(x, ys)
+
+    def mul_exp2(self, x, exp):
+        """PaillierMulExp2: x^(2^y) mod n^2, y >= 0 (paillier.cc:615-719)."""
+        x = self._cipher(x)
+        ys = _scalar_list(exp, x.shape)
+        x, ys = _broadcast_scalar(x, ys)
+        if any(y < 0 for y in ys):
+            raise errors.InvalidArgumentError("y should be a positive tensor.")
+        return self._powm(x, [1 << y for y in ys])
+
+
+def _scalar_list(s, shape):
+    if isinstance(s, torch.Tensor):
+        return [int(v) for v in s.reshape(-1).cpu().tolist()], tuple(s.shape)
+    a = np.asarray(s)
+    return [int(v) for v in a.reshape(-1).tolist()], a.shape
+
+
+def _broadcast_shape(a, b):
+    return tuple(np.broadcast_shapes(tuple(a), tuple(b)))
+
+
+def _broadcast_pair(x: CipherTensor, y: CipherTensor):
+    shape = _broadcast_shape(x.shape, y.shape)
+    return _expand(x, shape), _expand(y, shape)
+
+
+def _expand(x: CipherTensor, shape) -> CipherTensor:
+    if x.shape == shape:
+        return x
+    idx = torch.arange(x.numel(), device=x.limbs.device).reshape(x.shape).expand(shape).reshape(-1)
+    return CipherTensor(x.limbs[idx].contiguous(), shape, x.key)
+
+
+def _broadcast_scalar(x: CipherTensor, ys_shape):
+    ys, yshape = ys_shape
+    shape = _broadcast_shape(x.shape, yshape)
+    x = _expand(x, shape)
+    ys = np.broadcast_to(np.array(ys, dtype=object).reshape(yshape), shape).reshape(-1).tolist()
+    return x, [int(v) for v in ys]
+
+
+# ----------------------------------------------------------------------------------------------
+# FixedPointTensor arithmetic with encrypted mantissas (paillier.py:116-145)
+# ----------------------------------------------------------------------------------------------
+
+def _fp_encode(v):
+    from efl.privacy.paillier import FixedPointTensor, fixedpoint_encode
+    return v if isinstance(v, FixedPointTensor) else fixedpoint_encode(v)
+
+
+def fixedpoint_add(self, another):
+    """FixedPointTensor.__add__ (paillier.py:116-133): align exponents with mul_exp2 shifts, then
+    add in ciphertext space; a plaintext side is encrypted with the other side's keypair."""
+    from efl.privacy.paillier import FixedPointTensor
+    another = _fp_encode(another)
+    se, ae = _efl_lib.as_tensor(self.exponent), _efl_lib.as_tensor(another.exponent)
+    dev = se.device if se.is_cuda else ae.device
+    se, ae = se.to(dev), ae.to(dev)
+    exponent = torch.minimum(se, ae)
+    d = se - ae
+    dl = torch.clamp(d, min=0)
+    dr = torch.abs(torch.clamp(d, max=0))
+    if not isinstance(self.mantissa, PaillierTensor):
+        self_m = another.mantissa.keypair.encrypt(self.mantissa)
+        another_m = another.mantissa
+    elif not isinstance(another.mantissa, PaillierTensor):
+        self_m = self.mantissa
+        another_m = self.mantissa.keypair.encrypt(another.mantissa)
+    else:
+        self_m, another_m = self.mantissa, another.mantissa
+    mantissa = (self_m << dl) + (another_m << dr)
+    return FixedPointTensor(mantissa, exponent)
+
+
+def fixedpoint_mul(self, another):
+    """FixedPointTensor.__mul__ (paillier.py:135-138): ciphertext ^ plaintext mantissa."""
+    from efl.privacy.paillier import FixedPointTensor
+    another = _fp_encode(another)
+    ex = _efl_lib.as_tensor(self.exponent)
+    ey = _efl_lib.as_tensor(another.exponent).to(ex.device)
+    return FixedPointTensor(self.mantissa * another.mantissa, ex + ey)
+
+
+def fixedpoint_matmul(self, another):
+    raise errors.UnimplementedError("PaillierMatmul needs the ciphertext inverse (not yet on GPU)")

@@ -117,6 +117,92 @@ int efl_fxp_decode_batched(const int64_t* const* mantissas, const int64_t* const
                            void* const* ys, int dtype, const int64_t* ns, int64_t count,
                            int64_t max_n, int flags, void* stream);
 
+
+/* ----------------------------------------------------------------------------------------- */
+/* Stage P — Paillier cipher                                                                  */
+/* ----------------------------------------------------------------------------------------- */
+
+/*
+ * Key context. The reference keeps it in the PaillierKeypair TF resource (paillier.cc:50-331:
+ * n, n^2, hs, max, fbpowm table; p, q, p^2, q^2, hp, hq, q^-1 mod p). Here the caller derives
+ * the same quantities (plus Montgomery constants), packs them as little-endian 32-bit limbs into
+ * ONE device buffer (the "key block") and describes it with this struct; the library never
+ * allocates. All big-number offsets are in 32-bit words from the start of the key block.
+ *   ln           limbs of n (16, 32, 64, 128 = 512..4096-bit n); n^2 has 2*ln limbs, p and q ln/2,
+ *                p^2 and q^2 ln limbs.
+ *   n2_minv      -n^2^-1 mod 2^32 (Montgomery), likewise p2_/q2_/p_/q_minv.
+ *   off_n2_r2    R^2 mod n^2, R = 2^(32*2*ln);  off_n2_one  R mod n^2
+ *   off_table    fbpowm table, table_rows x table_cols entries of 2*ln limbs, entry [i][j] =
+ *                hs^((j+1) * 2^(group_size*i)) * R mod n^2 (gmp_utils.cc:56-89, Montgomery form)
+ *   off_p2_r3    R'^3 mod p^2, R' = 2^(32*ln) (and q2)
+ *   off_pm1      exponent p-1 (ln/2 limbs, pm1_bits significant bits), likewise q-1
+ *   off_pinv_w   p^-1 mod 2^(32*ln/2) (exact division by p), likewise q
+ *   off_hp       hp * R'' mod p with R'' = 2^(32*ln/2), hp = h-function (paillier.cc:28-37)
+ *   off_qinvp    (q^-1 mod p) * R'' mod p
+ *   off_max      ceil(2n/3) (paillier.cc:76-77), ln limbs
+ */
+typedef struct {
+  int32_t ln;
+  int32_t a_bits;
+  int32_t group_size;
+  int32_t table_rows;
+  int32_t table_cols;
+  int32_t has_private;
+  int32_t pm1_bits;
+  int32_t qm1_bits;
+  uint32_t n2_minv, p2_minv, q2_minv, p_minv, q_minv;
+  int64_t off_n, off_n2, off_n2_r2, off_n2_one, off_table, off_max;
+  int64_t off_p, off_q, off_p2, off_q2, off_p2_r3, off_q2_r3, off_pm1, off_qm1;
+  int64_t off_pinv_w, off_qinv_w, off_hp, off_hq, off_qinvp;
+} efl_pl_key;
+
+/*
+ * PaillierEncrypt (paillier.cc:443-503, Keypair::Encrypt :103-131): ciphertext[i] (2*ln limbs)
+ * = (1 + |m| n)^(sign) * hsa mod n^2. hsa: [n][2*ln] limbs, or NULL for the reference's
+ * hsa == "0" case: a fresh a of a_bits bits per element from Philox4x32-10(key = seed, counter =
+ * counter_base + i) and hsa = hs^(a') through the fixed-base table (a' = a with every
+ * group_size-bit group bit-reversed, as mpz_fbpowm does). n of up to 2048 bits.
+ */
+int efl_pl_encrypt(const void* key_block, const efl_pl_key* key, const int64_t* plaintext,
+                   const uint32_t* hsa, uint32_t* ciphertext, int64_t n, uint64_t seed,
+                   int64_t counter_base, void* stream);
+
+/* FixedBasePowm::mpz_fbpowm (gmp_utils.cc:107-144): hsa[i] = hs^(a_i') mod n^2 for a given
+ * [n][ceil(a_bits/32)] (or, a == NULL, the Philox draw of efl_pl_encrypt). */
+int efl_pl_fbpowm(const void* key_block, const efl_pl_key* key, const uint32_t* a, uint32_t* hsa,
+                  int64_t n, uint64_t seed, int64_t counter_base, void* stream);
+
+/*
+ * PaillierDecrypt (paillier.cc:505-561, _Decrypt :296-312): CRT decryption of [n][2*ln]
+ * ciphertexts into |m| ([n][ln] limbs) and negative[i] = (m < 0) where m > ceil(2n/3) maps to
+ * m - n. ABORTED "No private key." without p, q. n of up to 4096 bits.
+ */
+int efl_pl_decrypt(const void* key_block, const efl_pl_key* key, const uint32_t* ciphertext,
+                   uint32_t* magnitude, int8_t* negative, int64_t n, void* stream);
+
+/* PaillierAdd (paillier.cc:157-178, :563-613): z = x * y mod n^2. */
+int efl_pl_add(const void* key_block, const efl_pl_key* key, const uint32_t* x, const uint32_t* y,
+               uint32_t* z, int64_t n, void* stream);
+
+/* z = x^e mod n^2 with a per-element non-negative exponent of exp_words 32-bit words
+ * (PaillierMulScalar / PaillierMulExp2, paillier.cc:180-265, 615-719). */
+int efl_pl_powm(const void* key_block, const efl_pl_key* key, const uint32_t* x, const uint32_t* exps,
+                int exp_words, uint32_t* z, int64_t n, void* stream);
+
+/* mpz_get_str(..., 16) of n numbers ([n][limbs_per_elem], optional sign bytes): first the text
+ * lengths (efl_hex_lengths), then, given offsets = exclusive prefix sum (n + 1 entries), the
+ * characters (efl_hex_write). */
+int efl_hex_lengths(const uint32_t* limbs, int limbs_per_elem, const int8_t* negative,
+                    int64_t* lengths, int64_t n, void* stream);
+int efl_hex_write(const uint32_t* limbs, int limbs_per_elem, const int8_t* negative,
+                  const int64_t* offsets, char* chars, int64_t n, void* stream);
+/* mpz_set_str(..., 16) of n texts "[-]hexdigits" into limbs; bad <- -1 or the first bad index. */
+int efl_hex_parse(const char* chars, const int64_t* offsets, int limbs_per_elem, uint32_t* limbs,
+                  int8_t* negative, int64_t n, int64_t* bad, void* stream);
+/* PaillierDecrypt<int64> output: mpz_get_sll (gmp_utils.cc:38-45): low 64 bits of |m|, signed. */
+int efl_pl_to_int64(const uint32_t* magnitude, int limbs_per_elem, const int8_t* negative,
+                    int64_t* out, int64_t n, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,212 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY (see fxp_oracle.c header).
+ *
+ * Paillier arithmetic of efls-train through GMP 6.2.1, in the reference's own call order, used to
+ * pin the Python-int restatement (oracle/paillier.py) and to produce the golden known-answer
+ * vectors in tests/golden/ (the reference ships none: efls-train/test/paillier_test.py uses fresh
+ * time-seeded keys and allclose). Restated from:
+ *   keygen   GeneratePaillierKeypairOp::Compute   efls-train/cc/efl/math/paillier.cc:833-904
+ *   keys     SetPublicKey / SetPrivateKey         paillier.cc:70-101, h-function :28-37
+ *   encrypt  PaillierKeypair::Encrypt             paillier.cc:103-131 (hsa given)
+ *   decrypt  _Decrypt + m-function                paillier.cc:296-312, :39-48
+ *   fbpowm   FixedBasePowm::init_table/mpz_fbpowm gmp_utils.cc:56-144
+ * Strings are lowercase hex as mpz_get_str(..., 16) writes them (gmp_utils.cc:146-150).
+ */
+#include <gmp.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define EFL_EXPORT __attribute__((visibility("default")))
+
+static void put(char* out, size_t cap, const mpz_t v) {
+  char* s = mpz_get_str(NULL, 16, v);
+  strncpy(out, s, cap - 1);
+  out[cap - 1] = 0;
+  void (*freefunc)(void*, size_t);
+  mp_get_memory_functions(NULL, NULL, &freefunc);
+  freefunc(s, strlen(s) + 1);
+}
+
+/* keygen with an explicit MT seed (the reference seeds with time(), paillier.cc:845-849) */
+static void draw_prime(mpz_t r, gmp_randstate_t st, int bits, int reps) {
+  do {
+    mpz_urandomb(r, st, (mp_bitcnt_t)bits);
+    mpz_setbit(r, 0);
+    mpz_setbit(r, 1);
+    mpz_setbit(r, (mp_bitcnt_t)(bits - 1));
+  } while (!mpz_probab_prime_p(r, reps));
+}
+
+EFL_EXPORT void pl_gmp_keygen(int n_bytes, int reps, unsigned long seed, char* n_out, char* hs_out,
+                              char* p_out, char* q_out, size_t cap) {
+  mpz_t p, q, n, hs, t1, t2;
+  gmp_randstate_t st;
+  mpz_inits(p, q, n, hs, t1, t2, NULL);
+  gmp_randinit_mt(st);
+  gmp_randseed_ui(st, seed);
+  const int bits = n_bytes * 4;                           /* paillier.cc:852 n_bytes << 2 */
+  for (;;) {                                              /* gcd(p-1, q-1) must be 2 */
+    draw_prime(p, st, bits, reps);
+    draw_prime(q, st, bits, reps);
+    mpz_sub_ui(t1, p, 1);
+    mpz_sub_ui(t2, q, 1);
+    mpz_gcd(t1, t1, t2);
+    if (mpz_cmp_ui(t1, 2) == 0) break;
+  }
+  mpz_mul(n, p, q);
+  do {                                                    /* x in Z_n^* */
+    mpz_urandomm(t1, st, n);
+    mpz_gcd(t2, t1, n);
+  } while (mpz_cmp_ui(t2, 1) != 0);
+  mpz_mul(hs, t1, t1);                                    /* hs = (-x^2)^n mod n^2 */
+  mpz_neg(hs, hs);
+  mpz_mod(hs, hs, n);
+  mpz_mul(t1, n, n);
+  mpz_powm(hs, hs, n, t1);
+  put(n_out, cap, n);
+  put(hs_out, cap, hs);
+  put(p_out, cap, p);
+  put(q_out, cap, q);
+  mpz_clears(p, q, n, hs, t1, t2, NULL);
+  gmp_randclear(st);
+}
+
+/* Encrypt given hsa (non-zero): c = (1 + |m| n)^(+-1) * hsa mod n^2 */
+EFL_EXPORT void pl_gmp_encrypt(const char* n_hex, long long m, const char* hsa_hex, char* out, size_t cap) {
+  mpz_t n, n2, c, h;
+  mpz_inits(n, n2, c, h, NULL);
+  mpz_set_str(n, n_hex, 16);
+  mpz_mul(n2, n, n);
+  mpz_set_str(h, hsa_hex, 16);
+  unsigned long long u = m < 0 ? 0ull - (unsigned long long)m : (unsigned long long)m;
+  mpz_import(c, 1, -1, sizeof(u), 0, 0, &u);
+  mpz_mul(c, c, n);
+  mpz_add_ui(c, c, 1);
+  if (m < 0) mpz_invert(c, c, n2);
+  mpz_mul(c, c, h);
+  mpz_mod(c, c, n2);
+  put(out, cap, c);
+  mpz_clears(n, n2, c, h, NULL);
+}
+
+/* h(x) = (L_x((n+1)^(x-1) mod x^2))^-1 mod x */
+static void h_func(mpz_t r, const mpz_t n, const mpz_t x, const mpz_t x2) {
+  mpz_t g;
+  mpz_init(g);
+  mpz_add_ui(g, n, 1);
+  mpz_sub_ui(r, x, 1);
+  mpz_powm(r, g, r, x2);
+  mpz_sub_ui(r, r, 1);
+  mpz_divexact(r, r, x);
+  mpz_invert(r, r, x);
+  mpz_clear(g);
+}
+
+/* m_x(c) = L_x(c^(x-1) mod x^2) * h mod x */
+static void m_func(mpz_t r, const mpz_t c, const mpz_t x, const mpz_t x2, const mpz_t h) {
+  mpz_t e;
+  mpz_init(e);
+  mpz_sub_ui(e, x, 1);
+  mpz_powm(r, c, e, x2);
+  mpz_sub_ui(r, r, 1);
+  mpz_divexact(r, r, x);
+  mpz_mul(r, r, h);
+  mpz_mod(r, r, x);
+  mpz_clear(e);
+}
+
+EFL_EXPORT void pl_gmp_decrypt(const char* p_hex, const char* q_hex, const char* c_hex, char* out, size_t cap) {
+  mpz_t p, q, n, p2, q2, hp, hq, qinv, mx, c, m, cq;
+  mpz_inits(p, q, n, p2, q2, hp, hq, qinv, mx, c, m, cq, NULL);
+  mpz_set_str(p, p_hex, 16);
+  mpz_set_str(q, q_hex, 16);
+  mpz_mul(n, p, q);
+  mpz_mul(p2, p, p);
+  mpz_mul(q2, q, q);
+  h_func(hp, n, p, p2);
+  h_func(hq, n, q, q2);
+  mpz_invert(qinv, q, p);
+  mpz_mul_2exp(mx, n, 1);                                /* max = ceil(2n/3), paillier.cc:76-77 */
+  mpz_cdiv_q_ui(mx, mx, 3);
+  mpz_set_str(c, c_hex, 16);
+  m_func(m, c, p, p2, hp);
+  m_func(cq, c, q, q2, hq);
+  mpz_sub(m, m, cq);                                      /* CRT */
+  mpz_mul(m, m, qinv);
+  mpz_mod(m, m, p);
+  mpz_mul(m, m, q);
+  mpz_add(m, m, cq);
+  mpz_mod(m, m, n);
+  if (mpz_cmp(m, mx) > 0) mpz_sub(m, m, n);
+  put(out, cap, m);
+  mpz_clears(p, q, n, p2, q2, hp, hq, qinv, mx, c, m, cq, NULL);
+}
+
+/* fixed-base powm through the reference's table and lookup order */
+EFL_EXPORT int pl_gmp_fbpowm(const char* base_hex, const char* mod_hex, unsigned exp_bits, unsigned g,
+                             const char* a_hex, char* out, size_t cap) {
+  mpz_t base, mod, a, acc;
+  mpz_inits(base, mod, a, acc, NULL);
+  mpz_set_str(base, base_hex, 16);
+  mpz_set_str(mod, mod_hex, 16);
+  mpz_set_str(a, a_hex, 16);
+  const unsigned long long cols = (1ull << g) - 1;
+  const unsigned rows = exp_bits / g + (exp_bits % g ? 1 : 0);
+  mpz_t* T = (mpz_t*)malloc(sizeof(mpz_t) * rows * cols);
+  for (unsigned long long i = 0; i < rows * cols; ++i) mpz_init(T[i]);
+  /* row 0: base^1 .. base^cols; row i: row i-1 raised to 2^g */
+  mpz_set(T[0], base);
+  for (unsigned long long j = 1; j < cols; ++j) {
+    mpz_mul(T[j], T[j - 1], base);
+    mpz_mod(T[j], T[j], mod);
+  }
+  for (unsigned i = 1; i < rows; ++i)
+    for (unsigned long long j = 0; j < cols; ++j)
+      mpz_powm_ui(T[i * cols + j], T[(i - 1) * cols + j], 1ul << g, mod);
+  int rc = 1;
+  size_t size = mpz_sizeinbase(a, 2);
+  if (mpz_sgn(a) == 0) size = 1;                         /* sizeinbase(0) = 1 */
+  if (size > exp_bits) {
+    rc = -1;
+  } else {
+    mpz_set_ui(acc, 1);
+    const size_t full = size / g;
+    for (size_t i = 0; i < full; ++i) {
+      unsigned long idx = 0;
+      for (unsigned j = 0; j < g; ++j) idx = (idx << 1) | (unsigned long)mpz_tstbit(a, i * g + j);
+      if (idx) {
+        mpz_mul(acc, acc, T[i * cols + idx - 1]);
+        mpz_mod(acc, acc, mod);
+      }
+    }
+    if (size % g) {
+      unsigned long idx = 0;
+      for (size_t b = full * g; b < size; ++b) idx = (idx << 1) | (unsigned long)mpz_tstbit(a, b);
+      /* the reference indexes with --idx unconditionally here (gmp_utils.cc:133-137): the top
+       * partial group holds the leading 1 bit of a, so idx >= 1 — except a == 0 with g > 1, an
+       * out-of-bounds read in the reference (probability 2^-a_bits); defined here as a^0 = 1. */
+      if (idx) {
+        mpz_mul(acc, acc, T[full * cols + idx - 1]);
+        mpz_mod(acc, acc, mod);
+      }
+    }
+    put(out, cap, acc);
+  }
+  for (unsigned long long i = 0; i < rows * cols; ++i) mpz_clear(T[i]);
+  free(T);
+  mpz_clears(base, mod, a, acc, NULL);
+  return rc;
+}
+
+/* plain powm, for spot checks */
+EFL_EXPORT void pl_gmp_powm(const char* b_hex, const char* e_hex, const char* m_hex, char* out, size_t cap) {
+  mpz_t b, e, m, r;
+  mpz_inits(b, e, m, r, NULL);
+  mpz_set_str(b, b_hex, 16);
+  mpz_set_str(e, e_hex, 16);
+  mpz_set_str(m, m_hex, 16);
+  mpz_powm(r, b, e, m);
+  put(out, cap, r);
+  mpz_clears(b, e, m, r, NULL);
+}

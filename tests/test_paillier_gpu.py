@@ -1,0 +1,163 @@
+"""GPU parity of Stage P (libefl_hip.so csrc/paillier.hip) against GMP-made known answers and the
+Python-int oracle. Bar: bit-exact ciphertext hex given hsa; exact decryption; exact fbpowm."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import paillier as P
+from oracle import philox
+
+pytestmark = pytest.mark.gpu
+
+with open(os.path.join(GOLDEN, "paillier_kat.json")) as f:
+    KAT = json.load(f)
+ENC_KEYS = [k for k in KAT["keys"] if k["n_bytes"] <= 128]       # encrypt on GPU: n <= 2048 bits
+ALL = KAT["keys"]
+
+
+@pytest.fixture(scope="module")
+def efl():
+    import efl as _efl
+    _efl.lib.require_gpu()
+    return _efl
+
+
+def keypair(efl, k, private=True, g=1, seed=1234):
+    kp = efl.paillier.Keypair(seed=seed)
+    kp.set_keys_ints(int(k["n"], 16), int(k["hs"], 16), k["a_bits"] // 8, g,
+                     int(k["p"], 16) if private else None, int(k["q"], 16) if private else None)
+    return kp
+
+
+def ids(k):
+    return f"n{8 * k['n_bytes']}"
+
+
+@pytest.mark.parametrize("k", [k for k in ALL if k["n_bytes"] <= 256], ids=ids)
+def test_encrypt_given_hsa_kat(efl, k):
+    if k["n_bytes"] > 128:
+        pytest.skip("encrypt on the GPU: n up to 2048 bits")
+    kp = keypair(efl, k)
+    vs = k["vectors"]
+    m = torch.tensor([v["m"] for v in vs], dtype=torch.int64, device="cuda")
+    ct = kp.encrypt(m, hsa=[v["hsa"] for v in vs])
+    assert ct.tensor.to_hex().strings() == [v["c"] for v in vs]
+
+
+@pytest.mark.parametrize("k", ALL, ids=ids)
+def test_decrypt_kat(efl, k):
+    kp = keypair(efl, k)
+    vs = k["vectors"]
+    hx = efl.HexTensor.from_strings([v["c"] for v in vs])
+    assert kp.decrypt(hx).strings() == [v["d"] for v in vs]
+    got = kp.decrypt(hx, dtype=torch.int64).cpu().tolist()
+    assert got == [v["m"] for v in vs]
+
+
+@pytest.mark.parametrize("k", ENC_KEYS, ids=ids)
+def test_fbpowm_kat(efl, k):
+    for g in sorted({v["g"] for v in k["vectors"]}):
+        kp = keypair(efl, k, g=g)
+        vs = [v for v in k["vectors"] if v["g"] == g]
+        out = kp.fbpowm(a=[int(v["a"], 16) for v in vs])
+        assert out.to_hex().strings() == [v["hsa"] for v in vs]
+
+
+@pytest.mark.parametrize("k", ENC_KEYS, ids=ids)
+def test_homomorphic_ops_kat(efl, k):
+    kp = keypair(efl, k)
+    c0 = efl.HexTensor.from_strings([k["vectors"][5]["c"]])
+    c1 = efl.HexTensor.from_strings([k["vectors"][6]["c"]])
+    assert kp.add(c0, c1).to_hex().strings() == [k["ops"]["add"]]
+    assert kp.mul_scalar(c0, 7).to_hex().strings() == [k["ops"]["mul_scalar_7"]]
+    assert kp.mul_exp2(c1, 5).to_hex().strings() == [k["ops"]["mul_exp2_5"]]
+
+
+@pytest.mark.parametrize("g", [1, 3])
+def test_encrypt_random_a_is_philox_stream(efl, g):
+    """hsa == 0 path: a = Philox(seed, counter_base + i); c == oracle encrypt with hs^(a')."""
+    k = ENC_KEYS[0]
+    kp = keypair(efl, k, g=g, seed=0xC0FFEE)
+    okp = P.Keypair(int(k["n"], 16), int(k["hs"], 16), k["a_bits"] // 8, g, int(k["p"], 16), int(k["q"], 16))
+    rng = random.Random(g)
+    ms = [rng.randrange(-2**63, 2**63) for _ in range(70)]
+    ct = kp.encrypt(torch.tensor(ms), counter_base=1000)
+    got = ct.tensor.to_hex().strings()
+    for i, m in enumerate(ms):
+        a = philox.draw_a(0xC0FFEE, 1000 + i, k["a_bits"])
+        want = P.encrypt(okp, m, P.fbpowm(okp.hs, okp.n2, a, g))
+        assert got[i] == P.hx(want), i
+    assert kp.decrypt(ct, dtype=torch.int64).cpu().tolist() == ms
+
+
+def test_round_trip_and_counter_advance(efl):
+    k = ENC_KEYS[1]
+    kp = keypair(efl, k)
+    m = torch.randint(-2**62, 2**62, (33, 7), dtype=torch.int64)
+    a = kp.encrypt(m)
+    b = kp.encrypt(m)                        # fresh randomness: different ciphertexts
+    assert kp.counter == 2 * m.numel()
+    assert a.tensor.to_hex().strings() != b.tensor.to_hex().strings()
+    assert torch.equal(kp.decrypt(a, dtype=torch.int64).cpu(), m)
+    assert torch.equal(kp.decrypt(b, dtype="int64").cpu(), m)
+    d = kp.decrypt(a)                        # default: hex strings
+    assert d.shape == (33, 7) and [int(s, 16) for s in d.strings()] == m.reshape(-1).tolist()
+
+
+def test_errors(efl):
+    k = ENC_KEYS[0]
+    pub = keypair(efl, k, private=False)
+    ct = pub.encrypt(torch.tensor([1, 2, 3]))
+    with pytest.raises(efl.errors.AbortedError, match="No private key"):
+        pub.decrypt(ct)
+    with pytest.raises(efl.errors.AbortedError, match="No public key"):
+        efl.paillier.Keypair().encrypt(torch.tensor([1]))
+    with pytest.raises(efl.errors.InvalidArgumentError, match="same size"):
+        pub.encrypt(torch.tensor([1, 2]), hsa=["1"])
+    with pytest.raises(efl.errors.InvalidArgumentError, match="hex"):
+        pub.add(efl.HexTensor.from_strings(["12", "zz"]), efl.HexTensor.from_strings(["1", "1"]))
+    with pytest.raises(efl.errors.InvalidArgumentError, match="positive"):
+        pub.mul_exp2(ct, torch.tensor([1, -1, 2]))
+
+
+def test_fixed_point_encrypt_decrypt_like_reference_test(efl):
+    """efls-train/test/paillier_test.py:20-31 (encode -> encrypt -> decrypt -> decode), 1024-bit."""
+    kp = efl.paillier.Keypair()
+    kp.generate_keypair(n_bytes=128)
+    a = torch.randn(100, 100, generator=torch.Generator().manual_seed(0)).cuda()
+    b = efl.paillier.fixedpoint.encode(a)
+    b.mantissa = kp.encrypt(b.mantissa)
+    b.mantissa = b.mantissa.decrypt()
+    y = efl.paillier.fixedpoint.decode(b)
+    assert torch.equal(y[a != 0], a[a != 0])           # exact, stronger than the reference allclose
+
+
+def test_fixed_point_add_like_reference_test(efl):
+    """paillier_test.py:33-47: encrypted a + plaintext b (mul_exp2 alignment + PaillierAdd)."""
+    kp = efl.paillier.Keypair()
+    kp.generate_keypair(n_bytes=128)
+    g = torch.Generator().manual_seed(1)
+    a = torch.randn(40, 30, generator=g).cuda()
+    b = torch.randn(40, 30, generator=g).cuda()
+    fa = efl.paillier.fixedpoint.encode(a)
+    fa.mantissa = kp.encrypt(fa.mantissa)
+    c2 = fa + b
+    c2.mantissa = c2.mantissa.decrypt()
+    c2 = efl.paillier.fixedpoint.decode(c2)
+    c1 = (a.double() + b.double()).float()
+    assert torch.allclose(c1, c2)
+    # bit-exact: the exact integer sum (mantissas aligned like paillier.py:119-132) through the
+    # GMP-pinned hex decode of the oracle
+    from oracle import fxp
+    Ma, Ea = fxp.encode(a.cpu().numpy())
+    Mb, Eb = fxp.encode(b.cpu().numpy())
+    E = np.minimum(Ea, Eb).reshape(-1)
+    sums = [int(ma) * 2 ** int(ea - e) + int(mb) * 2 ** int(eb - e)
+            for ma, ea, mb, eb, e in zip(Ma.reshape(-1), Ea.reshape(-1), Mb.reshape(-1), Eb.reshape(-1), E)]
+    want = fxp.decode_hex([P.hx(v) for v in sums], E)
+    assert np.array_equal(c2.cpu().numpy().reshape(-1).view(np.uint32), want.view(np.uint32))
