@@ -163,6 +163,10 @@ class KeyBlock:
         if ln is None:
             raise errors.UnimplementedError(f"n of {n.bit_length()} bits: at most 4096 supported")
         self.ln, self.lc, self.lh = ln, 2 * ln, ln // 2
+        if a_bits <= 0 or a_bits > 32 * self.lc:
+            raise errors.InvalidArgumentError(f"a_bytes must be in [1, {4 * self.lc}] for this key")
+        if group_size < 1 or group_size > 20:
+            raise errors.InvalidArgumentError("group_size must be in [1, 20]")
         self.device = device or _efl_lib.require_gpu()
         self.desc = PlKey()
         words = []
@@ -455,6 +459,8 @@ class PaillierKeypair(object):
         if a is not None:
             a = list(a)
             n = len(a)
+            if any(v < 0 or v.bit_length() > k.a_bits for v in a):
+                raise errors.InvalidArgumentError("exponent wider than the fixed-base table")
             arr = np.stack([_limbs(v, words) for v in a]) if n else np.zeros((0, words), "<u4")
             a_dev = torch.from_numpy(arr.view(np.int32)).to(k.device)
         out = torch.empty((n, k.lc), dtype=torch.int32, device=k.device)
