@@ -107,7 +107,7 @@ def _probable_prime(x: int, reps: int, rng) -> bool:
         d //= 2
         s += 1
     for _ in range(reps):
-        a = 2 + rng.randbelow(x - 3)
+        a = rng.randrange(2, x - 1)
         y = pow(a, d, x)
         if y in (1, x - 1):
             continue
