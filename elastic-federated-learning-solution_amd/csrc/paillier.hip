@@ -439,6 +439,219 @@ __global__ __launch_bounds__(kPlBlock) void k_powm(Key k, const uint32_t* __rest
 }
 
 // ------------------------------------------------------------------------------------------
+// x^-1 mod n^2 (mpz_invert, paillier.cc:267-285) by binary extended Euclid on an odd modulus:
+// invariants A x = u, C x = v (mod M); u, v, A, C live in the lane's LDS columns (4 x LC words).
+// Trailing zeros are stripped k bits at a time with a Montgomery step (A + ((A*minv) mod 2^k) M is
+// divisible by 2^k). Bounded loop; a non-invertible x yields 0 and reports its index.
+// ------------------------------------------------------------------------------------------
+template <int L>
+struct LdsNum {
+  uint32_t* p;
+  int S;
+  __device__ __forceinline__ uint32_t& operator[](int j) const { return p[j * S]; }
+};
+
+template <int L>
+__device__ __forceinline__ bool lds_is_zero(const LdsNum<L>& x) {
+  uint32_t o = 0;
+  for (int j = 0; j < L; ++j) o |= x[j];
+  return o == 0;
+}
+
+// x >>= k (0 < k < 32)
+template <int L>
+__device__ __forceinline__ void lds_shr(const LdsNum<L>& x, int k) {
+  uint32_t lo = x[0];
+  for (int j = 0; j < L - 1; ++j) {
+    const uint32_t hi = x[j + 1];
+    x[j] = (lo >> k) | (hi << (32 - k));
+    lo = hi;
+  }
+  x[L - 1] = lo >> k;
+}
+
+// A <- A * 2^-k mod M (A < M, 0 < k < 32)
+template <int L>
+__device__ __forceinline__ void lds_half_k(const LdsNum<L>& A, int k, const uint32_t* __restrict__ M, uint32_t minv) {
+  const uint32_t t = (A[0] * minv) & ((1u << k) - 1u);
+  // A + t*M  (L+1 limbs), then >> k
+  uint32_t c = 0;
+  uint32_t prev = 0;
+  for (int j = 0; j < L; ++j) {
+    const uint64_t s = mad(t, M[j], (uint64_t)A[j] + c);
+    const uint32_t w = (uint32_t)s;
+    c = (uint32_t)(s >> 32);
+    if (j) A[j - 1] = (prev >> k) | (w << (32 - k));
+    prev = w;
+  }
+  A[L - 1] = (prev >> k) | (c << (32 - k));
+}
+
+// x >= y
+template <int L>
+__device__ __forceinline__ bool lds_geq(const LdsNum<L>& x, const LdsNum<L>& y) {
+  for (int j = L - 1; j >= 0; --j) {
+    const uint32_t a = x[j], b = y[j];
+    if (a != b) return a > b;
+  }
+  return true;
+}
+
+// x -= y (x >= y)
+template <int L>
+__device__ __forceinline__ void lds_sub(const LdsNum<L>& x, const LdsNum<L>& y) {
+  uint32_t br = 0;
+  for (int j = 0; j < L; ++j) {
+    const uint64_t d = (uint64_t)x[j] - y[j] - br;
+    x[j] = (uint32_t)d;
+    br = (uint32_t)(d >> 63);
+  }
+}
+
+// x = x - y mod M (x, y < M)
+template <int L>
+__device__ __forceinline__ void lds_modsub(const LdsNum<L>& x, const LdsNum<L>& y, const uint32_t* __restrict__ M) {
+  uint32_t br = 0;
+  for (int j = 0; j < L; ++j) {
+    const uint64_t d = (uint64_t)x[j] - y[j] - br;
+    x[j] = (uint32_t)d;
+    br = (uint32_t)(d >> 63);
+  }
+  if (br) {
+    uint32_t c = 0;
+    for (int j = 0; j < L; ++j) {
+      const uint64_t s = (uint64_t)x[j] + M[j] + c;
+      x[j] = (uint32_t)s;
+      c = (uint32_t)(s >> 32);
+    }
+  }
+}
+
+template <int LN>
+__global__ __launch_bounds__(kPlBlock) void k_invert(Key k, const uint32_t* __restrict__ x,
+                                                     uint32_t* __restrict__ out, long long N,
+                                                     unsigned long long* bad) {
+  constexpr int LC = 2 * LN;
+  extern __shared__ uint32_t lds[];
+  const int S = blockDim.x;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const uint32_t* M = k.at(k.d.off_n2);
+  const uint32_t minv = k.d.n2_minv;
+  LdsNum<LC> u{lds + threadIdx.x, S}, v{lds + LC * S + threadIdx.x, S};
+  LdsNum<LC> A{lds + 2 * LC * S + threadIdx.x, S}, C{lds + 3 * LC * S + threadIdx.x, S};
+  const uint32_t* xi = x + i * LC;
+  for (int j = 0; j < LC; ++j) {
+    u[j] = xi[j];
+    v[j] = M[j];
+    A[j] = j == 0 ? 1u : 0u;
+    C[j] = 0u;
+  }
+  // reduce u mod M first (inputs are ciphertexts < M; a single conditional subtract suffices)
+  bool ok = false;
+  const int max_iter = 4 * 32 * LC + 64;
+  for (int it = 0; it < max_iter; ++it) {
+    if (lds_is_zero<LC>(u)) {
+      // gcd in v; invertible iff v == 1
+      bool one = v[0] == 1u;
+      for (int j = 1; j < LC && one; ++j) one = v[j] == 0u;
+      ok = one;
+      break;
+    }
+    uint32_t w = u[0];
+    while (!(w & 1u)) {
+      const int kk = w ? __builtin_ctz(w) : 31;
+      const int sh = kk > 31 ? 31 : kk;
+      lds_shr<LC>(u, sh);
+      lds_half_k<LC>(A, sh, M, minv);
+      w = u[0];
+    }
+    w = v[0];
+    while (!(w & 1u)) {
+      const int kk = w ? __builtin_ctz(w) : 31;
+      const int sh = kk > 31 ? 31 : kk;
+      lds_shr<LC>(v, sh);
+      lds_half_k<LC>(C, sh, M, minv);
+      w = v[0];
+    }
+    if (lds_geq<LC>(u, v)) {
+      lds_sub<LC>(u, v);
+      lds_modsub<LC>(A, C, M);
+    } else {
+      lds_sub<LC>(v, u);
+      lds_modsub<LC>(C, A, M);
+    }
+  }
+  uint32_t* o = out + i * LC;
+  for (int j = 0; j < LC; ++j) o[j] = ok ? C[j] : 0u;
+  if (!ok) atomicMin(bad, (unsigned long long)i);
+}
+
+// PaillierMatmul core (paillier.cc:941-1051): one lane per output (i, k). Terms with y >= 0 are
+// multiplied into `pos`, terms with y < 0 (the reference's (x^-1)^|y|) into `neg`; the caller
+// finishes z = pos * neg^-1, the same group element the reference's ordered product gives.
+// Each term is (x^|y|)^(2^(xe + ye - min)).
+template <int LN>
+__global__ __launch_bounds__(kPlBlock) void k_matmul(Key k, const uint32_t* __restrict__ X,
+                                                     const long long* __restrict__ xe,
+                                                     const long long* __restrict__ ym,
+                                                     const long long* __restrict__ ye,
+                                                     uint32_t* __restrict__ zpos, uint32_t* __restrict__ zneg,
+                                                     long long* __restrict__ ze, int u, int v, int w) {
+  constexpr int LC = 2 * LN;
+  extern __shared__ uint32_t lds[];
+  const int S = blockDim.x;
+  uint32_t* acol = lds + threadIdx.x;
+  uint32_t* bcol = lds + LC * S + threadIdx.x;
+  uint32_t* pcol = lds + 2 * LC * S + threadIdx.x;   // running positive product (Montgomery)
+  const long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= (long long)u * w) return;
+  const int i = (int)(o / w), kk = (int)(o % w);
+  const uint32_t* n2 = k.at(k.d.off_n2);
+  const uint32_t* one = k.at(k.d.off_n2_one);
+  long long mn = 0x7FFFFFFFFFFFFFFFll;
+  for (int j = 0; j < v; ++j) {
+    const long long e = xe[(long long)i * v + j] + ye[(long long)j * w + kk];
+    mn = e < mn ? e : mn;
+  }
+  uint32_t t[LC], neg[LC];
+  load_uniform<LC>(t, one);
+  to_lds<LC>(pcol, S, t);
+  load_uniform<LC>(neg, one);
+  for (int j = 0; j < v; ++j) {
+    const long long y = ym[(long long)j * w + kk];
+    if (y == 0) continue;                                     // x^0 = 1
+    const uint64_t ay = y < 0 ? 0ull - (uint64_t)y : (uint64_t)y;
+    const long long delta = xe[(long long)i * v + j] + ye[(long long)j * w + kk] - mn;
+    // base = x_ij * R
+    load_g<LC>(t, X + ((long long)i * v + j) * LC);
+    mont_mul<LC>(t, Uniform{k.at(k.d.off_n2_r2)}, n2, k.d.n2_minv);
+    to_lds<LC>(bcol, S, t);
+    const int bits = 64 - __clzll((long long)ay);
+    for (int b = bits - 2; b >= 0; --b) {
+      mont_sqr<LC>(t, acol, S, n2, k.d.n2_minv);
+      if ((ay >> b) & 1ull) mont_mul<LC>(t, LdsCol{bcol, S}, n2, k.d.n2_minv);
+    }
+    for (long long d = 0; d < delta; ++d) mont_sqr<LC>(t, acol, S, n2, k.d.n2_minv);
+    if (y > 0) {
+      mont_mul<LC>(t, LdsCol{pcol, S}, n2, k.d.n2_minv);
+      to_lds<LC>(pcol, S, t);
+    } else {
+      to_lds<LC>(bcol, S, neg);
+      mont_mul<LC>(t, LdsCol{bcol, S}, n2, k.d.n2_minv);
+      copy<LC>(neg, t);
+    }
+  }
+  // back to normal form
+  for (int j = 0; j < LC; ++j) t[j] = pcol[j * S];
+  redc<LC>(t, n2, k.d.n2_minv);
+  store_g<LC>(zpos + o * LC, t);
+  redc<LC>(neg, n2, k.d.n2_minv);
+  store_g<LC>(zneg + o * LC, neg);
+  ze[o] = mn;
+}
+
+// ------------------------------------------------------------------------------------------
 // limbs <-> hex text (mpz_get_str(..., 16) / mpz_set_str(..., 16))
 // ------------------------------------------------------------------------------------------
 
@@ -579,6 +792,25 @@ struct RunPowm {
   }
 };
 
+template <int LN>
+struct RunInvert {
+  static hipError_t run(Key k, const uint32_t* x, uint32_t* out, long long N, unsigned long long* bad, hipStream_t s) {
+    const size_t lds = (size_t)4 * (2 * LN) * kPlBlock * 4;
+    hipLaunchKernelGGL((k_invert<LN>), dim3(grid_of(N)), dim3(kPlBlock), lds, s, k, x, out, N, bad);
+    return hipGetLastError();
+  }
+};
+template <int LN>
+struct RunMatmul {
+  static hipError_t run(Key k, const uint32_t* X, const long long* xe, const long long* ym, const long long* ye,
+                        uint32_t* zpos, uint32_t* zneg, long long* ze, int u, int v, int w, hipStream_t s) {
+    const size_t lds = (size_t)3 * (2 * LN) * kPlBlock * 4;
+    hipLaunchKernelGGL((k_matmul<LN>), dim3(grid_of((long long)u * w)), dim3(kPlBlock), lds, s, k, X, xe, ym, ye,
+                       zpos, zneg, ze, u, v, w);
+    return hipGetLastError();
+  }
+};
+
 template <int LP>
 hipError_t run_decrypt(Key k, const uint32_t* ct, uint32_t* mag, signed char* neg, long long N, hipStream_t s) {
   const size_t lds = (size_t)2 * LP * kPlBlock * 4;
@@ -650,6 +882,32 @@ EFL_API int efl_pl_powm(const void* key_block, const efl_pl_key* key, const uint
   Key k{(const uint32_t*)key_block, *key};
   return hip_status(dispatch_ln<RunPowm>(key->ln, k, x, exps, exp_words, z, (long long)n, (hipStream_t)stream),
                     "efl_pl_powm");
+}
+
+EFL_API int efl_pl_invert(const void* key_block, const efl_pl_key* key, const uint32_t* x, uint32_t* z,
+                          int64_t n, int64_t* bad, void* stream) {
+  if (!key_ok(key, false, 64)) return EFL_E_INVALID_ARGUMENT;
+  if (!bad) { set_error("null status word"); return EFL_E_INVALID_ARGUMENT; }
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = hipMemsetAsync(bad, 0xFF, sizeof(int64_t), s);
+  if (e != hipSuccess || n <= 0) return n < 0 ? EFL_E_INVALID_ARGUMENT : hip_status(e, "efl_pl_invert");
+  Key k{(const uint32_t*)key_block, *key};
+  return hip_status(dispatch_ln<RunInvert>(key->ln, k, x, z, (long long)n, (unsigned long long*)bad, s),
+                    "efl_pl_invert");
+}
+
+EFL_API int efl_pl_matmul(const void* key_block, const efl_pl_key* key, const uint32_t* x_mantissa,
+                          const int64_t* x_exponent, const int64_t* y_mantissa, const int64_t* y_exponent,
+                          uint32_t* z_pos, uint32_t* z_neg, int64_t* z_exponent, int u, int v, int w,
+                          void* stream) {
+  if (!key_ok(key, false, 64)) return EFL_E_INVALID_ARGUMENT;
+  if (u < 0 || v <= 0 || w < 0) { set_error("bad matmul shape"); return EFL_E_INVALID_ARGUMENT; }
+  if ((long long)u * w == 0) return EFL_OK;
+  Key k{(const uint32_t*)key_block, *key};
+  return hip_status(dispatch_ln<RunMatmul>(key->ln, k, x_mantissa, (const long long*)x_exponent,
+                                            (const long long*)y_mantissa, (const long long*)y_exponent, z_pos,
+                                            z_neg, (long long*)z_exponent, u, v, w, (hipStream_t)stream),
+                    "efl_pl_matmul");
 }
 
 EFL_API int efl_hex_lengths(const uint32_t* limbs, int limbs_per_elem, const int8_t* negative,

@@ -313,6 +313,10 @@ class Communicator(object):
     # client side ---------------------------------------------------------------------
     def _send_raw(self, name, t):
         from efl.privacy.hex_tensor import HexTensor
+        if hasattr(t, "tensor") and hasattr(t, "keypair"):      # PaillierTensor
+            t = t.tensor
+        if hasattr(t, "to_hex"):                                  # CipherTensor: DT_STRING on the wire
+            t = t.to_hex()
         if isinstance(t, HexTensor):
             dtype, shape, content = wire.DT_STRING, t.shape, t.to_tensor_content()
         else:

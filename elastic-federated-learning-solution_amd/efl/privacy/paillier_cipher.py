@@ -52,6 +52,8 @@ for _name, _args in {
     "efl_hex_write": [_vp, _i32, _vp, _vp, _vp, _i64, _vp],
     "efl_hex_parse": [_vp, _vp, _i32, _vp, _vp, _i64, _vp, _vp],
     "efl_pl_to_int64": [_vp, _i32, _vp, _vp, _i64, _vp],
+    "efl_pl_invert": [_vp, _PK, _vp, _vp, _i64, _vp, _vp],
+    "efl_pl_matmul": [_vp, _PK, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _vp],
 }.items():
     getattr(_lib, _name).argtypes = _args
     getattr(_lib, _name).restype = _i32
@@ -511,14 +513,64 @@ class PaillierKeypair(object):
                                         _stream(k.device)))
         return CipherTensor(out, x.shape, k)
 
+    def invert(self, x):
+        """PaillierInvert: x^-1 mod n^2 (paillier.cc:267-285, 721-797)."""
+        k = self.key
+        x = self._cipher(x)
+        out = torch.empty_like(x.limbs)
+        bad = torch.empty(1, dtype=torch.int64, device=k.device)
+        _efl_lib.check(_lib.efl_pl_invert(*k.args(), x.limbs.data_ptr(), out.data_ptr(), x.numel(),
+                                          bad.data_ptr(), _stream(k.device)))
+        b = int(bad.item())
+        if b >= 0:
+            raise errors.InvalidArgumentError(f"element {b} has no inverse mod n^2")
+        return CipherTensor(out, x.shape, k)
+
     def mul_scalar(self, x, scalar):
-        """PaillierMulScalar: x^y mod n^2 (negative y through the inverse, paillier.cc:180-265)."""
+        """PaillierMulScalar: x^y mod n^2; for y < 0 the reference computes (x^-1)^|y|
+        (paillier.cc:180-265), the same element as (x^|y|)^-1, which is what runs here."""
         x = self._cipher(x)
         ys = _scalar_list(scalar, x.shape)
         x, ys = _broadcast_scalar(x, ys)
-        if any(y < 0 for y in ys):
-            raise errors.UnimplementedError("negative scalars need the ciphertext inverse (not yet on GPU)")
-        return self._powm(x, ys)
+        z = self._powm(x, [abs(y) for y in ys])
+        negs = [i for i, y in enumerate(ys) if y < 0]
+        if negs:
+            idx = torch.tensor(negs, dtype=torch.int64, device=z.limbs.device)
+            zi = self.invert(CipherTensor(z.limbs[idx].contiguous(), (len(negs),), z.key))
+            z.limbs[idx] = zi.limbs
+        return z
+
+    def matmul(self, xm, xe, ym, ye):
+        """PaillierMatmul (paillier.cc:915-1053): ciphertext [u, v] x plaintext fixed-point [v, w]
+        -> (ciphertext mantissa [u, w], exponent [u, w])."""
+        k = self.key
+        x = self._cipher(xm)
+        xe = _efl_lib.as_tensor(xe).to(k.device, torch.int64).contiguous()
+        ym = _efl_lib.as_tensor(ym).to(k.device, torch.int64).contiguous()
+        ye = _efl_lib.as_tensor(ye).to(k.device, torch.int64).contiguous()
+        if len(x.shape) != 2:
+            raise errors.InvalidArgumentError("the rank of x should be two.")
+        if ym.dim() != 2:
+            raise errors.InvalidArgumentError("the rank of y should be two.")
+        if tuple(xe.shape) != x.shape:
+            raise errors.InvalidArgumentError("x_mantissa and x_exponent should be the same size.")
+        if ym.shape != ye.shape:
+            raise errors.InvalidArgumentError("y_mantissa and y_exponent should be the same size.")
+        u, v = x.shape
+        if ym.shape[0] != v:
+            raise errors.InvalidArgumentError("the size of x's 1st dim should be equal to the size of y's 2nd dim.")
+        w = ym.shape[1]
+        zpos = torch.empty((u * w, k.lc), dtype=torch.int32, device=k.device)
+        zneg = torch.empty_like(zpos)
+        ze = torch.empty((u, w), dtype=torch.int64, device=k.device)
+        _efl_lib.check(_lib.efl_pl_matmul(*k.args(), x.limbs.data_ptr(), xe.data_ptr(), ym.data_ptr(), ye.data_ptr(),
+                                          zpos.data_ptr(), zneg.data_ptr(), ze.data_ptr(), u, v, w,
+                                          _stream(k.device)))
+        if bool((ym < 0).any()):
+            inv = self.invert(CipherTensor(zneg, (u * w,), k))
+            z = self.add(CipherTensor(zpos, (u * w,), k), inv)
+            return CipherTensor(z.limbs, (u, w), k), ze
+        return CipherTensor(zpos, (u, w), k), ze
 
     def mul_exp2(self, x, exp):
         """PaillierMulExp2: x^(2^y) mod n^2, y >= 0 (paillier.cc:615-719)."""
@@ -604,4 +656,9 @@ def fixedpoint_mul(self, another):
 
 
 def fixedpoint_matmul(self, another):
-    raise errors.UnimplementedError("PaillierMatmul needs the ciphertext inverse (not yet on GPU)")
+    """FixedPointTensor.__matmul__ (paillier.py:140-145) -> PaillierMatmul."""
+    from efl.privacy.paillier import FixedPointTensor
+    another = _fp_encode(another)
+    keypair = self.mantissa.keypair
+    mantissa, exponent = keypair.matmul(self.mantissa.tensor, self.exponent, another.mantissa, another.exponent)
+    return FixedPointTensor(PaillierTensor(keypair, mantissa), exponent)

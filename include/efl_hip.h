@@ -189,6 +189,20 @@ int efl_pl_add(const void* key_block, const efl_pl_key* key, const uint32_t* x, 
 int efl_pl_powm(const void* key_block, const efl_pl_key* key, const uint32_t* x, const uint32_t* exps,
                 int exp_words, uint32_t* z, int64_t n, void* stream);
 
+/* PaillierInvert (paillier.cc:267-285, :721-797): z = x^-1 mod n^2 (binary extended Euclid on the
+ * GPU). bad <- -1, or the first index without an inverse (its z is 0). */
+int efl_pl_invert(const void* key_block, const efl_pl_key* key, const uint32_t* x, uint32_t* z,
+                  int64_t n, int64_t* bad, void* stream);
+
+/* PaillierMatmul (paillier.cc:915-1053) core: x_mantissa [u][v] ciphertexts, x_exponent [u][v],
+ * y_mantissa / y_exponent [v][w] int64. For each output z_exponent = min_j(xe + ye) and the terms
+ * (x^|y|)^(2^(xe + ye - min)) are multiplied into z_pos (y > 0) or z_neg (y < 0); the caller
+ * finishes z = z_pos * z_neg^-1 (efl_pl_invert + efl_pl_add). */
+int efl_pl_matmul(const void* key_block, const efl_pl_key* key, const uint32_t* x_mantissa,
+                  const int64_t* x_exponent, const int64_t* y_mantissa, const int64_t* y_exponent,
+                  uint32_t* z_pos, uint32_t* z_neg, int64_t* z_exponent, int u, int v, int w,
+                  void* stream);
+
 /* mpz_get_str(..., 16) of n numbers ([n][limbs_per_elem], optional sign bytes): first the text
  * lengths (efl_hex_lengths), then, given offsets = exclusive prefix sum (n + 1 entries), the
  * characters (efl_hex_write). */

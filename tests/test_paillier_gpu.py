@@ -161,3 +161,63 @@ def test_fixed_point_add_like_reference_test(efl):
             for ma, ea, mb, eb, e in zip(Ma.reshape(-1), Ea.reshape(-1), Mb.reshape(-1), Eb.reshape(-1), E)]
     want = fxp.decode_hex([P.hx(v) for v in sums], E)
     assert np.array_equal(c2.cpu().numpy().reshape(-1).view(np.uint32), want.view(np.uint32))
+
+
+def test_invert_and_negative_scalars(efl):
+    k = ENC_KEYS[1]
+    kp = keypair(efl, k)
+    okp = P.Keypair(int(k["n"], 16), int(k["hs"], 16), k["a_bits"] // 8, 1, int(k["p"], 16), int(k["q"], 16))
+    cs = [int(v["c"], 16) for v in k["vectors"][:12]]
+    hx = efl.HexTensor.from_ints(cs)
+    assert kp.invert(hx).to_hex().to_ints() == [P.invert(okp, c) for c in cs]
+    ys = [3, -1, 0, -7, 2**40 + 1, -(2**62), 5, -2, 1, -1, 9, -2**63]
+    got = kp.mul_scalar(hx, torch.tensor(ys)).to_hex().to_ints()
+    assert got == [P.mul_scalar(okp, c, y) for c, y in zip(cs, ys)]
+    with pytest.raises(efl.errors.InvalidArgumentError, match="no inverse"):
+        kp.invert(efl.HexTensor.from_ints([okp.n]))         # gcd(n, n^2) != 1
+
+
+def test_matmul_vs_oracle(efl):
+    k = ENC_KEYS[0]
+    kp = keypair(efl, k)
+    okp = P.Keypair(int(k["n"], 16), int(k["hs"], 16), k["a_bits"] // 8, 1, int(k["p"], 16), int(k["q"], 16))
+    rng = np.random.default_rng(5)
+    u, v, w = 3, 5, 4
+    xm_plain = rng.integers(-2**20, 2**20, (u, v))
+    ct = kp.encrypt(torch.from_numpy(xm_plain))
+    xe = rng.integers(-30, -10, (u, v))
+    ym = rng.integers(-2**20, 2**20, (v, w))
+    ym[0, 0] = 0
+    ye = rng.integers(-25, -12, (v, w))
+    zm, ze = kp.matmul(ct.tensor, torch.from_numpy(xe), torch.from_numpy(ym), torch.from_numpy(ye))
+    xs = [[int(s, 16) for s in row] for row in np.array(ct.tensor.to_hex().strings()).reshape(u, v)]
+    om, oe = P.matmul(okp, xs, xe.tolist(), ym.tolist(), ye.tolist())
+    assert np.array_equal(ze.cpu().numpy(), np.array(oe))
+    assert zm.to_hex().to_ints() == [c for row in om for c in row]
+    # and the plaintext meaning: sum_j xm*ym*2^(xe+ye-min)
+    dec = kp.decrypt(zm, dtype="string").to_ints()
+    want = [sum(int(xm_plain[i, j]) * int(ym[j, q]) * 2 ** int(xe[i, j] + ye[j, q] - oe[i][q]) for j in range(v))
+            for i in range(u) for q in range(w)]
+    assert dec == want
+
+
+def test_fixed_point_matmul_and_mul_like_reference_test(efl):
+    """paillier_test.py:49-79 (mul_scalar, matmul) with a 512-bit key; exact plaintext check."""
+    kp = efl.paillier.Keypair()
+    kp.generate_keypair(n_bytes=64)
+    g = torch.Generator().manual_seed(2)
+    a = torch.randn(6, 5, generator=g).cuda()
+    b = torch.randn(6, 5, generator=g).cuda()
+    fa = efl.paillier.fixedpoint.encode(a)
+    fa.mantissa = kp.encrypt(fa.mantissa)
+    c2 = fa * b
+    c2.mantissa = c2.mantissa.decrypt()
+    c2 = efl.paillier.fixedpoint.decode(c2)
+    assert torch.allclose(a * b, c2)
+    bm = torch.randn(5, 3, generator=g).cuda()
+    fa = efl.paillier.fixedpoint.encode(a)
+    fa.mantissa = kp.encrypt(fa.mantissa)
+    c3 = fa @ bm
+    c3.mantissa = c3.mantissa.decrypt()
+    c3 = efl.paillier.fixedpoint.decode(c3)
+    assert torch.allclose(a @ bm, c3, 1e-5, 1e-4)
