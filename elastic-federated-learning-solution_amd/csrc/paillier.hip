@@ -189,8 +189,9 @@ __global__ __launch_bounds__(kPlBlock) void k_encrypt(Key k, const long long* __
   constexpr int LC = 2 * LN;
   extern __shared__ uint32_t lds[];
   const int S = blockDim.x;
-  uint32_t* acol = lds + threadIdx.x;
-  uint32_t* bcol = lds + LC * S + threadIdx.x;
+  const int awords = (k.d.a_bits + 31) >> 5;
+  uint32_t* acol = lds + threadIdx.x;                               // a (or squaring scratch)
+  uint32_t* bcol = lds + (awords > LC ? awords : LC) * S + threadIdx.x;
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N) return;
   const uint32_t* n = k.at(k.d.off_n);
@@ -220,11 +221,11 @@ __global__ __launch_bounds__(kPlBlock) void k_fbpowm(Key k, const uint32_t* __re
   constexpr int LC = 2 * LN;
   extern __shared__ uint32_t lds[];
   const int S = blockDim.x;
+  const int words = (k.d.a_bits + 31) >> 5;
   uint32_t* acol = lds + threadIdx.x;
-  uint32_t* bcol = lds + LC * S + threadIdx.x;
+  uint32_t* bcol = lds + (words > LC ? words : LC) * S + threadIdx.x;
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N) return;
-  const int words = (k.d.a_bits + 31) >> 5;
   if (a_in) {
     for (int w = 0; w < words; ++w) acol[w * S] = a_in[i * words + w];
   } else {
@@ -732,6 +733,7 @@ __global__ __launch_bounds__(256) void k_to_int64(const uint32_t* __restrict__ m
 
 inline bool key_ok(const efl_pl_key* d, bool need_private, int ln_max) {
   if (!d) { set_error("null key descriptor"); return false; }
+  if (d->a_bits <= 0 || d->a_bits > 8192) { set_error("a_bits must be in [1, 8192]"); return false; }
   if (d->ln != 16 && d->ln != 32 && d->ln != 64 && d->ln != 128) {
     set_error("unsupported limb count %d (n of 512/1024/2048/4096 bits)", d->ln);
     return false;
@@ -760,7 +762,8 @@ template <int LN>
 struct RunEncrypt {
   static hipError_t run(Key k, const long long* m, const uint32_t* hsa, uint32_t* out, long long N,
                         uint64_t seed, long long ctr0, hipStream_t s) {
-    const size_t lds = (size_t)2 * (2 * LN) * kPlBlock * 4;
+    const int aw = (k.d.a_bits + 31) / 32;
+    const size_t lds = (size_t)((aw > 2 * LN ? aw : 2 * LN) + 2 * LN) * kPlBlock * 4;
     hipLaunchKernelGGL((k_encrypt<LN>), dim3(grid_of(N)), dim3(kPlBlock), lds, s, k, m, hsa, out, N, seed, ctr0);
     return hipGetLastError();
   }
@@ -769,7 +772,8 @@ template <int LN>
 struct RunFbpowm {
   static hipError_t run(Key k, const uint32_t* a, uint32_t* out, long long N, uint64_t seed, long long ctr0,
                         hipStream_t s) {
-    const size_t lds = (size_t)2 * (2 * LN) * kPlBlock * 4;
+    const int aw = (k.d.a_bits + 31) / 32;
+    const size_t lds = (size_t)((aw > 2 * LN ? aw : 2 * LN) + 2 * LN) * kPlBlock * 4;
     hipLaunchKernelGGL((k_fbpowm<LN>), dim3(grid_of(N)), dim3(kPlBlock), lds, s, k, a, out, N, seed, ctr0);
     return hipGetLastError();
   }

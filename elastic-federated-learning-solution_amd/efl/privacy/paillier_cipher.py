@@ -165,8 +165,8 @@ class KeyBlock:
         if ln is None:
             raise errors.UnimplementedError(f"n of {n.bit_length()} bits: at most 4096 supported")
         self.ln, self.lc, self.lh = ln, 2 * ln, ln // 2
-        if a_bits <= 0 or a_bits > 32 * self.lc:
-            raise errors.InvalidArgumentError(f"a_bytes must be in [1, {4 * self.lc}] for this key")
+        if a_bits <= 0 or a_bits > 8192:
+            raise errors.InvalidArgumentError("a_bytes must be in [1, 1024]")
         if group_size < 1 or group_size > 20:
             raise errors.InvalidArgumentError("group_size must be in [1, 20]")
         self.device = device or _efl_lib.require_gpu()
