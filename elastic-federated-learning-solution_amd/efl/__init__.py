@@ -13,6 +13,7 @@ from efl.lib import set_flush_denormal, flush_denormal
 from efl.privacy import encryptor_utils
 from efl.privacy import paillier
 from efl.privacy import paillier_cipher
+from efl.privacy import paillier_layer
 from efl.privacy.hex_tensor import HexTensor
 from efl.framework import communicator
 from efl.framework import encrypt_hook

@@ -662,3 +662,55 @@ def fixedpoint_matmul(self, another):
     keypair = self.mantissa.keypair
     mantissa, exponent = keypair.matmul(self.mantissa.tensor, self.exponent, another.mantissa, another.exponent)
     return FixedPointTensor(PaillierTensor(keypair, mantissa), exponent)
+
+
+@exporter.export("paillier.Hook")
+class PaillierHook(object):
+    """Key exchange (paillier.py:158-205): the SENDER generates the keypair and sends the public
+    key [n, hs] and n_bytes; the RECEIVER installs it (group size 1, as paillier.py:69-70).
+    `after_create_session()` runs the exchange; `before_run/after_run` refresh every
+    `update_step_interval` steps."""
+
+    def __init__(self, keypair, communicator, role, prefix, update_step_interval=None, n_bytes=None,
+                 a_bytes=None, reps=None, group_size=None):
+        from efl.privacy.encryptor_utils import Role
+        self._kp, self._comm, self._role, self._prefix = keypair, communicator, role, prefix
+        self._interval = update_step_interval
+        self._local_step = 0
+        self._n_bytes = 512 if n_bytes is None else n_bytes
+        self._a_bytes = self._n_bytes // 2 if a_bytes is None else a_bytes
+        self._reps, self._group = reps, group_size
+        if role not in (Role.SENDER, Role.RECEIVER):
+            raise ValueError(str(role) + ": No such role.")
+        self._sender = role == Role.SENDER
+
+    def _update(self):
+        if self._sender:
+            public_key, _ = self._kp.generate_keypair(n_bytes=self._n_bytes, a_bytes=self._a_bytes, reps=self._reps,
+                                                      group_size=self._group)
+            return [self._comm.send(self._prefix + "_public_key", public_key),
+                    self._comm.send(self._prefix + "_bytes", torch.tensor([self._n_bytes], dtype=torch.int32))]
+        pk = self._comm.recv(self._prefix + "_public_key", shape=(2,), dtype="string")
+        nb = self._comm.recv(self._prefix + "_bytes", dtype=torch.int32)
+        s = pk.strings()
+        self._kp.set_public_key(s[0], nb, s[1], self._a_bytes, group_size=self._group)
+        return []
+
+    def after_create_session(self, sess=None, coord=None):
+        self._kp.initialize()
+        if self._interval is None:
+            for h in self._update():
+                h.result()
+
+    def before_run(self, run_context=None):
+        if self._interval is not None and self._local_step % self._interval == 0:
+            self._local_step = 0
+            for h in self._update():
+                h.result()
+
+    def after_run(self, run_context=None, run_values=None):
+        if self._interval is not None:
+            self._local_step += 1
+
+    def end(self, sess=None):
+        pass
