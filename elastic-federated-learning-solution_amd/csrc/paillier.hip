@@ -13,38 +13,16 @@
 // seed with counter = global element index (counter-based: independent of GPU count/launch shape).
 #include "bignum.h"
 #include "common.h"
+#include "pl_common.h"
 
 namespace efl {
 namespace {
 
 using namespace big;
+using pl::Key;
+using pl::philox;
 
 constexpr int kPlBlock = 64;   // one wave per workgroup: LDS columns are per lane
-
-struct Key {
-  const uint32_t* base;
-  efl_pl_key d;
-  __device__ __forceinline__ const uint32_t* at(int64_t off) const { return base + off; }
-};
-
-// ------------------------------------------------------------------------------------------
-// Philox4x32-10 (Salmon et al., SC'11): counter (ctr_lo, ctr_hi, block, 0), key = seed.
-// ------------------------------------------------------------------------------------------
-__device__ __forceinline__ void philox(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
-    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
-    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
-    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
-    c[0] = n0;
-    c[1] = (uint32_t)p1;
-    c[2] = n2;
-    c[3] = (uint32_t)p0;
-    k0 += 0x9E3779B9u;
-    k1 += 0xBB67AE85u;
-  }
-}
 
 // a = Philox stream of `words` 32-bit words for element counter ctr, written to an LDS column.
 __device__ __forceinline__ void draw_a(uint32_t* col, int S, int words, int a_bits, uint64_t seed,
@@ -746,6 +724,12 @@ inline bool key_ok(const efl_pl_key* d, bool need_private, int ln_max) {
   return true;
 }
 
+// kernel family per key size: 0 = one lane per element (paillier.hip), C = sliced over 2ln/C (n^2
+// ops) or ln/C (decryption) lanes of C limbs (paillier_sliced.hip). [ln 16/32/64/128][n^2 ops, decrypt]
+int g_slicing[4][2] = {{0, 0}, {0, 0}, {0, 0}, {32, 32}};
+inline int ln_index(int ln) { return ln == 16 ? 0 : ln == 32 ? 1 : ln == 64 ? 2 : 3; }
+inline int slicing(int ln, int dec) { return g_slicing[ln_index(ln)][dec]; }
+
 inline unsigned grid_of(long long N) { return (unsigned)((N + kPlBlock - 1) / kPlBlock); }
 
 template <template <int> class F, class... A>
@@ -797,13 +781,14 @@ struct RunPowm {
 };
 
 template <int LN>
-struct RunInvert {
-  static hipError_t run(Key k, const uint32_t* x, uint32_t* out, long long N, unsigned long long* bad, hipStream_t s) {
-    const size_t lds = (size_t)4 * (2 * LN) * kPlBlock * 4;
-    hipLaunchKernelGGL((k_invert<LN>), dim3(grid_of(N)), dim3(kPlBlock), lds, s, k, x, out, N, bad);
-    return hipGetLastError();
-  }
-};
+hipError_t run_invert(Key k, const uint32_t* x, uint32_t* out, long long N, unsigned long long* bad, hipStream_t s) {
+  // four LDS numbers per lane: 32 lanes per workgroup for n^2 of 8192 bits (128 KiB)
+  constexpr int block = LN >= 128 ? 32 : kPlBlock;
+  const size_t lds = (size_t)4 * (2 * LN) * block * 4;
+  hipLaunchKernelGGL((k_invert<LN>), dim3((unsigned)((N + block - 1) / block)), dim3(block), lds, s, k, x, out, N,
+                     bad);
+  return hipGetLastError();
+}
 template <int LN>
 struct RunMatmul {
   static hipError_t run(Key k, const uint32_t* X, const long long* xe, const long long* ym, const long long* ye,
@@ -830,7 +815,7 @@ using namespace efl;
 EFL_API int efl_pl_encrypt(const void* key_block, const efl_pl_key* key, const int64_t* plaintext,
                            const uint32_t* hsa, uint32_t* ciphertext, int64_t n, uint64_t seed,
                            int64_t counter_base, void* stream) {
-  if (!key_ok(key, false, 64)) return EFL_E_INVALID_ARGUMENT;
+  if (!key_ok(key, false, 128)) return EFL_E_INVALID_ARGUMENT;
   if (n < 0) { set_error("negative count"); return EFL_E_INVALID_ARGUMENT; }
   if (n == 0) return EFL_OK;
   if (!hsa && (key->table_rows <= 0 || key->group_size <= 0)) {
@@ -838,18 +823,23 @@ EFL_API int efl_pl_encrypt(const void* key_block, const efl_pl_key* key, const i
     return EFL_E_ABORTED;
   }
   Key k{(const uint32_t*)key_block, *key};
-  return hip_status(dispatch_ln<RunEncrypt>(key->ln, k, (const long long*)plaintext, hsa, ciphertext,
-                                             (long long)n, seed, (long long)counter_base, (hipStream_t)stream),
+  const int C = slicing(key->ln, 0);
+  return hip_status(C ? pl::sl_encrypt(k, C, (const long long*)plaintext, hsa, ciphertext, (long long)n, seed,
+                                       (long long)counter_base, (hipStream_t)stream)
+                      : dispatch_ln<RunEncrypt>(key->ln, k, (const long long*)plaintext, hsa, ciphertext,
+                                                (long long)n, seed, (long long)counter_base, (hipStream_t)stream),
                     "efl_pl_encrypt");
 }
 
 EFL_API int efl_pl_fbpowm(const void* key_block, const efl_pl_key* key, const uint32_t* a, uint32_t* hsa,
                           int64_t n, uint64_t seed, int64_t counter_base, void* stream) {
-  if (!key_ok(key, false, 64)) return EFL_E_INVALID_ARGUMENT;
+  if (!key_ok(key, false, 128)) return EFL_E_INVALID_ARGUMENT;
   if (n <= 0) return n < 0 ? EFL_E_INVALID_ARGUMENT : EFL_OK;
   Key k{(const uint32_t*)key_block, *key};
-  return hip_status(dispatch_ln<RunFbpowm>(key->ln, k, a, hsa, (long long)n, seed, (long long)counter_base,
-                                            (hipStream_t)stream),
+  const int C = slicing(key->ln, 0);
+  return hip_status(C ? pl::sl_fbpowm(k, C, a, hsa, (long long)n, seed, (long long)counter_base, (hipStream_t)stream)
+                      : dispatch_ln<RunFbpowm>(key->ln, k, a, hsa, (long long)n, seed, (long long)counter_base,
+                                               (hipStream_t)stream),
                     "efl_pl_fbpowm");
 }
 
@@ -861,6 +851,8 @@ EFL_API int efl_pl_decrypt(const void* key_block, const efl_pl_key* key, const u
   Key k{(const uint32_t*)key_block, *key};
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;
+  const int C = slicing(key->ln, 1);
+  if (C) return hip_status(pl::sl_decrypt(k, C, ciphertext, magnitude, (signed char*)negative, n, s), "efl_pl_decrypt");
   switch (key->ln) {
     case 16: e = run_decrypt<16>(k, ciphertext, magnitude, (signed char*)negative, n, s); break;
     case 32: e = run_decrypt<32>(k, ciphertext, magnitude, (signed char*)negative, n, s); break;
@@ -872,46 +864,78 @@ EFL_API int efl_pl_decrypt(const void* key_block, const efl_pl_key* key, const u
 
 EFL_API int efl_pl_add(const void* key_block, const efl_pl_key* key, const uint32_t* x, const uint32_t* y,
                        uint32_t* z, int64_t n, void* stream) {
-  if (!key_ok(key, false, 64)) return EFL_E_INVALID_ARGUMENT;
+  if (!key_ok(key, false, 128)) return EFL_E_INVALID_ARGUMENT;
   if (n <= 0) return n < 0 ? EFL_E_INVALID_ARGUMENT : EFL_OK;
   Key k{(const uint32_t*)key_block, *key};
-  return hip_status(dispatch_ln<RunAdd>(key->ln, k, x, y, z, (long long)n, (hipStream_t)stream), "efl_pl_add");
+  const int C = slicing(key->ln, 0);
+  return hip_status(C ? pl::sl_add(k, C, x, y, z, (long long)n, (hipStream_t)stream)
+                      : dispatch_ln<RunAdd>(key->ln, k, x, y, z, (long long)n, (hipStream_t)stream),
+                    "efl_pl_add");
 }
 
 EFL_API int efl_pl_powm(const void* key_block, const efl_pl_key* key, const uint32_t* x, const uint32_t* exps,
                         int exp_words, uint32_t* z, int64_t n, void* stream) {
-  if (!key_ok(key, false, 64)) return EFL_E_INVALID_ARGUMENT;
+  if (!key_ok(key, false, 128)) return EFL_E_INVALID_ARGUMENT;
   if (exp_words <= 0) { set_error("exp_words must be positive"); return EFL_E_INVALID_ARGUMENT; }
   if (n <= 0) return n < 0 ? EFL_E_INVALID_ARGUMENT : EFL_OK;
   Key k{(const uint32_t*)key_block, *key};
-  return hip_status(dispatch_ln<RunPowm>(key->ln, k, x, exps, exp_words, z, (long long)n, (hipStream_t)stream),
+  const int C = slicing(key->ln, 0);
+  return hip_status(C ? pl::sl_powm(k, C, x, exps, exp_words, z, (long long)n, (hipStream_t)stream)
+                      : dispatch_ln<RunPowm>(key->ln, k, x, exps, exp_words, z, (long long)n, (hipStream_t)stream),
                     "efl_pl_powm");
 }
 
 EFL_API int efl_pl_invert(const void* key_block, const efl_pl_key* key, const uint32_t* x, uint32_t* z,
                           int64_t n, int64_t* bad, void* stream) {
-  if (!key_ok(key, false, 64)) return EFL_E_INVALID_ARGUMENT;
+  if (!key_ok(key, false, 128)) return EFL_E_INVALID_ARGUMENT;
   if (!bad) { set_error("null status word"); return EFL_E_INVALID_ARGUMENT; }
   hipStream_t s = (hipStream_t)stream;
   hipError_t e = hipMemsetAsync(bad, 0xFF, sizeof(int64_t), s);
   if (e != hipSuccess || n <= 0) return n < 0 ? EFL_E_INVALID_ARGUMENT : hip_status(e, "efl_pl_invert");
   Key k{(const uint32_t*)key_block, *key};
-  return hip_status(dispatch_ln<RunInvert>(key->ln, k, x, z, (long long)n, (unsigned long long*)bad, s),
-                    "efl_pl_invert");
+  unsigned long long* b = (unsigned long long*)bad;
+  switch (key->ln) {
+    case 16: e = run_invert<16>(k, x, z, (long long)n, b, s); break;
+    case 32: e = run_invert<32>(k, x, z, (long long)n, b, s); break;
+    case 64: e = run_invert<64>(k, x, z, (long long)n, b, s); break;
+    default: e = run_invert<128>(k, x, z, (long long)n, b, s); break;
+  }
+  return hip_status(e, "efl_pl_invert");
 }
 
 EFL_API int efl_pl_matmul(const void* key_block, const efl_pl_key* key, const uint32_t* x_mantissa,
                           const int64_t* x_exponent, const int64_t* y_mantissa, const int64_t* y_exponent,
                           uint32_t* z_pos, uint32_t* z_neg, int64_t* z_exponent, int u, int v, int w,
                           void* stream) {
-  if (!key_ok(key, false, 64)) return EFL_E_INVALID_ARGUMENT;
+  if (!key_ok(key, false, 128)) return EFL_E_INVALID_ARGUMENT;
   if (u < 0 || v <= 0 || w < 0) { set_error("bad matmul shape"); return EFL_E_INVALID_ARGUMENT; }
   if ((long long)u * w == 0) return EFL_OK;
   Key k{(const uint32_t*)key_block, *key};
+  const int C = slicing(key->ln, 0);
+  if (C)
+    return hip_status(pl::sl_matmul(k, C, x_mantissa, (const long long*)x_exponent, (const long long*)y_mantissa,
+                                    (const long long*)y_exponent, z_pos, z_neg, (long long*)z_exponent, u, v, w,
+                                    (hipStream_t)stream),
+                      "efl_pl_matmul");
   return hip_status(dispatch_ln<RunMatmul>(key->ln, k, x_mantissa, (const long long*)x_exponent,
                                             (const long long*)y_mantissa, (const long long*)y_exponent, z_pos,
                                             z_neg, (long long*)z_exponent, u, v, w, (hipStream_t)stream),
                     "efl_pl_matmul");
+}
+
+EFL_API int efl_pl_tune(int ln, int decrypt, int limbs_per_lane) {
+  if (ln != 16 && ln != 32 && ln != 64 && ln != 128) { set_error("unsupported limb count %d", ln); return EFL_E_INVALID_ARGUMENT; }
+  const int dec = decrypt ? 1 : 0;
+  if (limbs_per_lane < 0) return slicing(ln, dec);   // query
+  if (limbs_per_lane == 0) {
+    if (!dec && ln > 64) { set_error("no one-lane kernels for n^2 of %d bits", 64 * ln); return EFL_E_INVALID_ARGUMENT; }
+  } else if (!pl::sliced_available(dec ? ln : 2 * ln, limbs_per_lane)) {
+    set_error("no sliced kernels with %d limbs per lane for %d-limb moduli", limbs_per_lane, dec ? ln : 2 * ln);
+    return EFL_E_INVALID_ARGUMENT;
+  }
+  const int prev = slicing(ln, dec);
+  g_slicing[ln_index(ln)][dec] = limbs_per_lane;
+  return prev;
 }
 
 EFL_API int efl_hex_lengths(const uint32_t* limbs, int limbs_per_elem, const int8_t* negative,

@@ -1,0 +1,557 @@
+// Stage P, sliced kernels: the Paillier ops for moduli too wide for one lane (n^2 of 2048/4096-bit
+// keys, p^2 of 4096-bit keys), and a lower-register alternative for 1024-bit keys.
+//
+// Reference: efls-train/cc/efl/math/paillier.cc — Encrypt :103-131, _Decrypt :296-312 with the
+// m/h-functions :28-48, Add/MulScalar/MulExp2 :157-265, Matmul :941-1051; fixed-base powm
+// gmp_utils.cc:107-144. Same algorithms, same outputs as paillier.hip's one-lane kernels (the
+// parity tests run both); only the data placement differs.
+//
+// One 64-lane wave per workgroup, G = L/C lanes per element, E = 64/G elements per workgroup.
+// Every element owns LDS arrays (limb i of array A at A[i*E]) for its b operands: squaring scratch,
+// the exponentiation base, the fixed-base table entry, running products. All G lanes read the
+// same word (broadcast); the E elements of the wave hit consecutive banks.
+#include "pl_common.h"
+#include "sliced.h"
+
+namespace efl {
+namespace pl {
+namespace {
+
+using namespace sl;
+
+constexpr int kSlBlock = 64;
+
+// lane's slice of a uniform number that has only `len` limbs (zero above)
+template <int C>
+__device__ __forceinline__ void slice_prefix(uint32_t (&x)[C], const uint32_t* __restrict__ p, int len, int g) {
+#pragma unroll
+  for (int j = 0; j < C; ++j) x[j] = g * C + j < len ? p[g * C + j] : 0u;
+}
+
+template <int C>
+__device__ __forceinline__ void from_lds(uint32_t (&x)[C], const uint32_t* base, int E, int g) {
+#pragma unroll
+  for (int j = 0; j < C; ++j) x[j] = base[(g * C + j) * E];
+}
+
+// the element's a (Philox stream, as paillier.hip's draw_a) into LDS; Philox blocks split over the group
+template <int G>
+__device__ __forceinline__ void draw_a(uint32_t* A, int E, int words, int a_bits, uint64_t seed, uint64_t ctr,
+                                       int g) {
+  const int rem = a_bits & 31;
+  for (int b = g; b * 4 < words; b += G) {
+    uint32_t c[4] = {(uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)b, 0u};
+    philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int w = b * 4 + j;
+      if (w < words) A[w * E] = (w == words - 1 && rem) ? c[j] & ((1u << rem) - 1u) : c[j];
+    }
+  }
+}
+
+// g = 1 + |m| n, or n^2 + 1 - |m| n for m < 0 (= (1 + |m| n)^-1 mod n^2), sliced over L = 2 ln limbs
+template <int C, int G>
+__device__ __forceinline__ void make_g(uint32_t (&t)[C], long long m, const Key& k, const uint32_t (&n2)[C],
+                                       int g) {
+  const uint64_t a = m < 0 ? 0ull - (uint64_t)m : (uint64_t)m;
+  const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32);
+  uint32_t ns[C];
+  slice_prefix<C>(ns, k.at(k.d.off_n), k.d.ln, g);
+  uint32_t c0 = 0;
+#pragma unroll
+  for (int j = 0; j < C; ++j) {
+    const uint64_t p = mad(a0, ns[j], c0);
+    t[j] = (uint32_t)p;
+    c0 = (uint32_t)(p >> 32);
+  }
+  uint32_t c1 = 0;
+#pragma unroll
+  for (int j = 0; j < C - 1; ++j) {
+    const uint64_t p = mad(a1, ns[j], (uint64_t)t[j + 1] + c1);
+    t[j + 1] = (uint32_t)p;
+    c1 = (uint32_t)(p >> 32);
+  }
+  const uint64_t top = mad(a1, ns[C - 1], c1);
+  // spill of this slice into the next lane: limb 0 += c0 + lo(top), limb 1 += hi(top)
+  uint32_t in0 = from_prev<G>(c0), in1 = from_prev<G>((uint32_t)top), in2 = from_prev<G>((uint32_t)(top >> 32));
+  if (g == 0) in0 = in1 = in2 = 0;
+  uint64_t s = (uint64_t)t[0] + in0 + in1;
+  t[0] = (uint32_t)s;
+  s = (uint64_t)t[1] + in2 + (s >> 32);
+  t[1] = (uint32_t)s;
+  uint32_t cc = (uint32_t)(s >> 32);
+#pragma unroll
+  for (int j = 2; j < C; ++j) {
+    s = (uint64_t)t[j] + cc;
+    t[j] = (uint32_t)s;
+    cc = (uint32_t)(s >> 32);
+  }
+  resolve_carries<C, G>(t, cc, g);
+  if (m < 0) rsub<C, G>(t, n2, g);
+  add_small<C, G>(t, 1u, g);
+}
+
+// hs^(a') R mod n^2 through the fixed-base table (gmp_utils.cc:107-144; see paillier.hip)
+template <int C, int G>
+__device__ __forceinline__ void fbpowm_mont(uint32_t (&acc)[C], const Key& k, const uint32_t* A, uint32_t* B, int E,
+                                            int words, const uint32_t (&n2)[C], int g) {
+  constexpr int L = C * G;
+  const int gs = k.d.group_size;
+  int size = 0;
+  for (int w = words - 1; w >= 0; --w) {
+    const uint32_t v = A[w * E];
+    if (v) { size = w * 32 + 32 - __clz(v); break; }
+  }
+  slice_uniform<C>(acc, k.at(k.d.off_n2_one), g);
+  const uint32_t* table = k.at(k.d.off_table);
+  const int cols = k.d.table_cols;
+  for (int s = 0, row = 0; s < size; s += gs, ++row) {
+    const int w = size - s < gs ? size - s : gs;
+    uint32_t idx = 0;
+    for (int j = 0; j < w; ++j) {
+      const int b = s + j;
+      idx = (idx << 1) | ((A[(b >> 5) * E] >> (b & 31)) & 1u);
+    }
+    if (idx) {
+      uint32_t ent[C];
+      load_slice<C>(ent, table + ((int64_t)row * cols + (idx - 1)) * L, g);
+      to_lds<C>(B, E, g, ent);
+      lds_sync();
+      mont_mul<C, G>(acc, LdsElem{B, E}, n2, k.d.n2_minv, g);
+    }
+  }
+}
+
+// Optional register cap (waves per SIMD) for the C = 16 / C = 32 kernels: build knob for tuning
+// (EFL_SL_WAVES16 / EFL_SL_WAVES32); default: the compiler's choice.
+#if defined(EFL_SL_WAVES16) && defined(EFL_SL_WAVES32)
+#define SL_OCC __attribute__((amdgpu_waves_per_eu(C == 16 ? EFL_SL_WAVES16 : EFL_SL_WAVES32)))
+#else
+#define SL_OCC
+#endif
+
+#define SL_ELEMENT(E_, G_)                                   \
+  const int g = (int)threadIdx.x % (G_);                     \
+  const int e = (int)threadIdx.x / (G_);                     \
+  const long long i = (long long)blockIdx.x * (E_) + e;
+
+// ------------------------------------------------------------------------------------------
+template <int C, int G>
+__global__ __launch_bounds__(kSlBlock) SL_OCC void k_encrypt(Key k, const long long* __restrict__ m,
+                                                      const uint32_t* __restrict__ hsa,
+                                                      uint32_t* __restrict__ out, long long N, uint64_t seed,
+                                                      long long ctr0) {
+  constexpr int L = C * G, E = kSlBlock / G;
+  extern __shared__ uint32_t lds[];
+  SL_ELEMENT(E, G)
+  if (i >= N) return;
+  const int words = (k.d.a_bits + 31) >> 5;
+  uint32_t* B = lds + e;
+  uint32_t* A = lds + L * E + e;
+  uint32_t n2[C];
+  slice_uniform<C>(n2, k.at(k.d.off_n2), g);
+  const uint32_t minv = k.d.n2_minv;
+  uint32_t c[C];
+  if (hsa) {
+    load_slice<C>(c, hsa + i * L, g);
+    to_lds<C>(B, E, g, c);
+    make_g<C, G>(c, m[i], k, n2, g);
+    lds_sync();
+    mont_mul<C, G>(c, LdsElem{B, E}, n2, minv, g);
+    mont_mul<C, G>(c, Uniform{k.at(k.d.off_n2_r2)}, n2, minv, g);
+  } else {
+    draw_a<G>(A, E, words, k.d.a_bits, seed, (uint64_t)(ctr0 + i), g);
+    lds_sync();
+    fbpowm_mont<C, G>(c, k, A, B, E, words, n2, g);
+    to_lds<C>(B, E, g, c);
+    make_g<C, G>(c, m[i], k, n2, g);
+    lds_sync();
+    mont_mul<C, G>(c, LdsElem{B, E}, n2, minv, g);
+  }
+  store_slice<C>(out + i * L, g, c);
+}
+
+template <int C, int G>
+__global__ __launch_bounds__(kSlBlock) SL_OCC void k_fbpowm(Key k, const uint32_t* __restrict__ a_in,
+                                                     uint32_t* __restrict__ out, long long N, uint64_t seed,
+                                                     long long ctr0) {
+  constexpr int L = C * G, E = kSlBlock / G;
+  extern __shared__ uint32_t lds[];
+  SL_ELEMENT(E, G)
+  if (i >= N) return;
+  const int words = (k.d.a_bits + 31) >> 5;
+  uint32_t* B = lds + e;
+  uint32_t* A = lds + L * E + e;
+  if (a_in) {
+    for (int w = g; w < words; w += G) A[w * E] = a_in[i * words + w];
+  } else {
+    draw_a<G>(A, E, words, k.d.a_bits, seed, (uint64_t)(ctr0 + i), g);
+  }
+  lds_sync();
+  uint32_t n2[C], acc[C];
+  slice_uniform<C>(n2, k.at(k.d.off_n2), g);
+  fbpowm_mont<C, G>(acc, k, A, B, E, words, n2, g);
+  redc<C, G>(acc, n2, k.d.n2_minv, g);
+  store_slice<C>(out + i * L, g, acc);
+}
+
+template <int C, int G>
+__global__ __launch_bounds__(kSlBlock) SL_OCC void k_add(Key k, const uint32_t* __restrict__ x,
+                                                  const uint32_t* __restrict__ y, uint32_t* __restrict__ out,
+                                                  long long N) {
+  constexpr int L = C * G, E = kSlBlock / G;
+  extern __shared__ uint32_t lds[];
+  SL_ELEMENT(E, G)
+  if (i >= N) return;
+  uint32_t* B = lds + e;
+  uint32_t n2[C], a[C];
+  slice_uniform<C>(n2, k.at(k.d.off_n2), g);
+  load_slice<C>(a, y + i * L, g);
+  to_lds<C>(B, E, g, a);
+  load_slice<C>(a, x + i * L, g);
+  lds_sync();
+  mont_mul<C, G>(a, LdsElem{B, E}, n2, k.d.n2_minv, g);
+  mont_mul<C, G>(a, Uniform{k.at(k.d.off_n2_r2)}, n2, k.d.n2_minv, g);
+  store_slice<C>(out + i * L, g, a);
+}
+
+template <int C, int G>
+__global__ __launch_bounds__(kSlBlock) SL_OCC void k_powm(Key k, const uint32_t* __restrict__ x,
+                                                   const uint32_t* __restrict__ exps, int ewords,
+                                                   uint32_t* __restrict__ out, long long N) {
+  constexpr int L = C * G, E = kSlBlock / G;
+  extern __shared__ uint32_t lds[];
+  SL_ELEMENT(E, G)
+  if (i >= N) return;
+  uint32_t* BASE = lds + e;
+  uint32_t* SCR = lds + L * E + e;
+  const uint32_t* ex = exps + i * ewords;
+  int ebits = 0;
+  for (int w = ewords - 1; w >= 0; --w)
+    if (ex[w]) { ebits = w * 32 + 32 - __clz(ex[w]); break; }
+  uint32_t t[C];
+  if (ebits == 0) {
+#pragma unroll
+    for (int j = 0; j < C; ++j) t[j] = (g == 0 && j == 0) ? 1u : 0u;
+    store_slice<C>(out + i * L, g, t);
+    return;
+  }
+  uint32_t n2[C];
+  slice_uniform<C>(n2, k.at(k.d.off_n2), g);
+  const uint32_t minv = k.d.n2_minv;
+  load_slice<C>(t, x + i * L, g);
+  mont_mul<C, G>(t, Uniform{k.at(k.d.off_n2_r2)}, n2, minv, g);
+  to_lds<C>(BASE, E, g, t);
+#pragma unroll 1
+  for (int b = ebits - 2; b >= 0; --b) {
+    mont_sqr<C, G>(t, SCR, E, n2, minv, g);
+    if ((ex[b >> 5] >> (b & 31)) & 1u) mont_mul<C, G>(t, LdsElem{BASE, E}, n2, minv, g);
+  }
+  redc<C, G>(t, n2, minv, g);
+  store_slice<C>(out + i * L, g, t);
+}
+
+// PaillierMatmul core, one group per output (see paillier.hip k_matmul)
+template <int C, int G>
+__global__ __launch_bounds__(kSlBlock) SL_OCC void k_matmul(Key k, const uint32_t* __restrict__ X,
+                                                     const long long* __restrict__ xe,
+                                                     const long long* __restrict__ ym,
+                                                     const long long* __restrict__ ye, uint32_t* __restrict__ zpos,
+                                                     uint32_t* __restrict__ zneg, long long* __restrict__ ze, int u,
+                                                     int v, int w) {
+  constexpr int L = C * G, E = kSlBlock / G;
+  extern __shared__ uint32_t lds[];
+  SL_ELEMENT(E, G)
+  const long long o = i;
+  if (o >= (long long)u * w) return;
+  const int row = (int)(o / w), kk = (int)(o % w);
+  uint32_t* BASE = lds + e;
+  uint32_t* SCR = lds + L * E + e;
+  uint32_t* POS = lds + 2 * L * E + e;
+  uint32_t* NEG = lds + 3 * L * E + e;
+  uint32_t n2[C], t[C];
+  slice_uniform<C>(n2, k.at(k.d.off_n2), g);
+  const uint32_t minv = k.d.n2_minv;
+  long long mn = 0x7FFFFFFFFFFFFFFFll;
+  for (int j = 0; j < v; ++j) {
+    const long long ex = xe[(long long)row * v + j] + ye[(long long)j * w + kk];
+    mn = ex < mn ? ex : mn;
+  }
+  slice_uniform<C>(t, k.at(k.d.off_n2_one), g);
+  to_lds<C>(POS, E, g, t);
+  to_lds<C>(NEG, E, g, t);
+  for (int j = 0; j < v; ++j) {
+    const long long y = ym[(long long)j * w + kk];
+    if (y == 0) continue;
+    const uint64_t ay = y < 0 ? 0ull - (uint64_t)y : (uint64_t)y;
+    const long long delta = xe[(long long)row * v + j] + ye[(long long)j * w + kk] - mn;
+    load_slice<C>(t, X + ((long long)row * v + j) * L, g);
+    mont_mul<C, G>(t, Uniform{k.at(k.d.off_n2_r2)}, n2, minv, g);
+    to_lds<C>(BASE, E, g, t);
+    const int bits = 64 - __clzll((long long)ay);
+    for (int b = bits - 2; b >= 0; --b) {
+      mont_sqr<C, G>(t, SCR, E, n2, minv, g);
+      if ((ay >> b) & 1ull) mont_mul<C, G>(t, LdsElem{BASE, E}, n2, minv, g);
+    }
+    for (long long d = 0; d < delta; ++d) mont_sqr<C, G>(t, SCR, E, n2, minv, g);
+    uint32_t* acc = y > 0 ? POS : NEG;
+    lds_sync();
+    mont_mul<C, G>(t, LdsElem{acc, E}, n2, minv, g);
+    to_lds<C>(acc, E, g, t);
+  }
+  lds_sync();
+  from_lds<C>(t, POS, E, g);
+  redc<C, G>(t, n2, minv, g);
+  store_slice<C>(zpos + o * L, g, t);
+  from_lds<C>(t, NEG, E, g);
+  redc<C, G>(t, n2, minv, g);
+  store_slice<C>(zneg + o * L, g, t);
+  if (g == 0) ze[o] = mn;
+}
+
+// ------------------------------------------------------------------------------------------
+// decryption: L = ln limbs (x^2 for x = p, q), half slices of C/2 limbs for numbers mod x
+// ------------------------------------------------------------------------------------------
+
+// res = L_x(c^(x-1) mod x^2) * h mod x   (paillier.cc:28-48)
+template <int C, int G>
+__device__ __forceinline__ void m_func(uint32_t (&res)[C / 2], const uint32_t* __restrict__ c, const Key& k,
+                                       bool second, uint32_t* BASE, uint32_t* SCR, int E, int g) {
+  constexpr int L = C * G, CH = C / 2, LH = L / 2;
+  uint32_t x2[C];
+  slice_uniform<C>(x2, k.at(second ? k.d.off_q2 : k.d.off_p2), g);
+  const uint32_t x2_minv = second ? k.d.q2_minv : k.d.p2_minv;
+  const uint32_t* r3 = k.at(second ? k.d.off_q2_r3 : k.d.off_p2_r3);
+  const uint32_t* ex = k.at(second ? k.d.off_qm1 : k.d.off_pm1);
+  const int ebits = second ? k.d.qm1_bits : k.d.pm1_bits;
+
+  // c R mod x^2 = hi R^2 + lo R  with c = hi 2^(32L) + lo
+  uint32_t t[C], lo[C];
+  load_slice<C>(t, c + L, g);
+  mont_mul<C, G>(t, Uniform{r3}, x2, x2_minv, g);   // hi R^2
+  load_slice<C>(lo, c, g);
+  mont_mul<C, G>(lo, Uniform{r3}, x2, x2_minv, g);  // lo R^2
+  redc<C, G>(lo, x2, x2_minv, g);                   // lo R
+  const uint32_t top = add<C, G>(t, lo, g);
+  csub<C, G>(t, x2, top != 0 || geq<C, G>(t, x2, g), g);
+  to_lds<C>(BASE, E, g, t);
+#pragma unroll 1
+  for (int b = ebits - 2; b >= 0; --b) {
+    mont_sqr<C, G>(t, SCR, E, x2, x2_minv, g);
+    if ((ex[b >> 5] >> (b & 31)) & 1u) mont_mul<C, G>(t, LdsElem{BASE, E}, x2, x2_minv, g);
+  }
+  redc<C, G>(t, x2, x2_minv, g);   // y = c^(x-1) mod x^2  (y = 1 mod x, so y >= 1)
+  sub_small<C, G>(t, 1u, g);
+  to_lds<C>(SCR, E, g, t);
+  lds_sync();
+  // (y - 1) / x exactly = (y - 1) * x^-1 mod 2^(32 LH): operand scanning, limb ii of the
+  // quotient leaves lane 0 after step ii
+  uint32_t xi[CH], q[CH];
+  slice_uniform<CH>(xi, k.at(second ? k.d.off_qinv_w : k.d.off_pinv_w), g);
+#pragma unroll
+  for (int j = 0; j < CH; ++j) q[j] = 0;
+  uint32_t pend = 0;
+#pragma unroll 1
+  for (int ii = 0; ii < LH; ++ii) {
+    const uint32_t yv = SCR[ii * E];
+    uint32_t c1 = 0;
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const uint64_t p = mad(xi[j], yv, (uint64_t)q[j] + c1);
+      q[j] = (uint32_t)p;
+      c1 = (uint32_t)(p >> 32);
+    }
+    if (g == 0) BASE[ii * E] = q[0];
+    uint32_t in = from_next<G>(q[0]);
+    if (g == G - 1) in = 0;
+#pragma unroll
+    for (int j = 0; j < CH - 1; ++j) q[j] = q[j + 1];
+    const uint64_t s = (uint64_t)in + pend + c1;
+    q[CH - 1] = (uint32_t)s;
+    pend = (uint32_t)(s >> 32);
+  }
+  lds_sync();
+  from_lds<CH>(q, BASE, E, g);
+  uint32_t xs[CH];
+  slice_uniform<CH>(xs, k.at(second ? k.d.off_q : k.d.off_p), g);
+  // * h mod x (h stored in Montgomery form -> normal result)
+  mont_mul<CH, G>(q, Uniform{k.at(second ? k.d.off_hq : k.d.off_hp)}, xs, second ? k.d.q_minv : k.d.p_minv, g);
+#pragma unroll
+  for (int j = 0; j < CH; ++j) res[j] = q[j];
+}
+
+template <int C, int G>
+__global__ __launch_bounds__(kSlBlock) SL_OCC void k_decrypt(Key k, const uint32_t* __restrict__ ct,
+                                                      uint32_t* __restrict__ mag, signed char* __restrict__ neg,
+                                                      long long N) {
+  constexpr int L = C * G, E = kSlBlock / G, CH = C / 2, LH = L / 2;
+  extern __shared__ uint32_t lds[];
+  SL_ELEMENT(E, G)
+  if (i >= N) return;
+  uint32_t* BASE = lds + e;
+  uint32_t* SCR = lds + L * E + e;
+  const uint32_t* c = ct + i * 2 * L;
+  uint32_t mp[CH], mq[CH];
+  m_func<C, G>(mp, c, k, false, BASE, SCR, E, g);
+  m_func<C, G>(mq, c, k, true, BASE, SCR, E, g);
+  // CRT (paillier.cc:296-307): h = ((mp - mq) mod p) * (q^-1 mod p) mod p; m = h q + mq
+  uint32_t ph[CH], qh[CH], d[CH];
+  slice_uniform<CH>(ph, k.at(k.d.off_p), g);
+  slice_uniform<CH>(qh, k.at(k.d.off_q), g);
+#pragma unroll
+  for (int j = 0; j < CH; ++j) d[j] = mq[j];
+  csub<CH, G>(d, ph, geq<CH, G>(d, ph, g), g);   // mq mod p (mq < q < 2p)
+  {
+    uint32_t r[CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) r[j] = mp[j];
+    if (sub<CH, G>(r, d, g)) add<CH, G>(r, ph, g);
+#pragma unroll
+    for (int j = 0; j < CH; ++j) d[j] = r[j];
+  }
+  mont_mul<CH, G>(d, Uniform{k.at(k.d.off_qinvp)}, ph, k.d.p_minv, g);
+  // m = h q + mq by operand scanning; low limbs leave lane 0 into SCR, the high half follows
+  to_lds<CH>(BASE, E, g, d);
+  lds_sync();
+  uint32_t t[CH];
+#pragma unroll
+  for (int j = 0; j < CH; ++j) t[j] = mq[j];
+  uint32_t pend = 0;
+#pragma unroll 1
+  for (int ii = 0; ii < LH; ++ii) {
+    const uint32_t hv = BASE[ii * E];
+    uint32_t c1 = 0;
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const uint64_t p = mad(qh[j], hv, (uint64_t)t[j] + c1);
+      t[j] = (uint32_t)p;
+      c1 = (uint32_t)(p >> 32);
+    }
+    if (g == 0) SCR[ii * E] = t[0];
+    uint32_t in = from_next<G>(t[0]);
+    if (g == G - 1) in = 0;
+#pragma unroll
+    for (int j = 0; j < CH - 1; ++j) t[j] = t[j + 1];
+    const uint64_t s = (uint64_t)in + pend + c1;
+    t[CH - 1] = (uint32_t)s;
+    pend = (uint32_t)(s >> 32);
+  }
+  resolve_carries<CH, G>(t, pend, g);
+#pragma unroll
+  for (int j = 0; j < CH; ++j) SCR[(LH + g * CH + j) * E] = t[j];
+  lds_sync();
+  uint32_t mm[C], ref[C];
+  from_lds<C>(mm, SCR, E, g);
+  // signed: m > max (= ceil(2n/3)) -> m - n  (paillier.cc:308-310)
+  slice_uniform<C>(ref, k.at(k.d.off_max), g);
+  const bool isneg = !geq<C, G>(ref, mm, g);
+  if (isneg) {
+    slice_uniform<C>(ref, k.at(k.d.off_n), g);
+    rsub<C, G>(mm, ref, g);
+  }
+  store_slice<C>(mag + i * L, g, mm);
+  if (g == 0) neg[i] = isneg ? 1 : 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------------
+inline unsigned grid_of(long long N, int G) {
+  const long long E = kSlBlock / G;
+  return (unsigned)((N + E - 1) / E);
+}
+
+template <int C, int G>
+hipError_t run_encrypt(const Key& k, const long long* m, const uint32_t* hsa, uint32_t* out, long long N,
+                       uint64_t seed, long long ctr0, hipStream_t s) {
+  const int aw = (k.d.a_bits + 31) / 32;
+  hipLaunchKernelGGL((k_encrypt<C, G>), dim3(grid_of(N, G)), dim3(kSlBlock), (size_t)(C * G + aw) * (kSlBlock / G) * 4, s, k, m,
+                     hsa, out, N, seed, ctr0);
+  return hipGetLastError();
+}
+template <int C, int G>
+hipError_t run_fbpowm(const Key& k, const uint32_t* a, uint32_t* out, long long N, uint64_t seed, long long ctr0,
+                      hipStream_t s) {
+  const int aw = (k.d.a_bits + 31) / 32;
+  hipLaunchKernelGGL((k_fbpowm<C, G>), dim3(grid_of(N, G)), dim3(kSlBlock), (size_t)(C * G + aw) * (kSlBlock / G) * 4, s, k, a,
+                     out, N, seed, ctr0);
+  return hipGetLastError();
+}
+template <int C, int G>
+hipError_t run_add(const Key& k, const uint32_t* x, const uint32_t* y, uint32_t* out, long long N, hipStream_t s) {
+  hipLaunchKernelGGL((k_add<C, G>), dim3(grid_of(N, G)), dim3(kSlBlock), (size_t)(C * G) * (kSlBlock / G) * 4, s, k, x, y, out, N);
+  return hipGetLastError();
+}
+template <int C, int G>
+hipError_t run_powm(const Key& k, const uint32_t* x, const uint32_t* e, int ew, uint32_t* out, long long N,
+                    hipStream_t s) {
+  hipLaunchKernelGGL((k_powm<C, G>), dim3(grid_of(N, G)), dim3(kSlBlock), (size_t)(2 * C * G) * (kSlBlock / G) * 4, s, k, x, e, ew,
+                     out, N);
+  return hipGetLastError();
+}
+template <int C, int G>
+hipError_t run_matmul(const Key& k, const uint32_t* X, const long long* xe, const long long* ym, const long long* ye,
+                      uint32_t* zpos, uint32_t* zneg, long long* ze, int u, int v, int w, hipStream_t s) {
+  hipLaunchKernelGGL((k_matmul<C, G>), dim3(grid_of((long long)u * w, G)), dim3(kSlBlock), (size_t)(4 * C * G) * (kSlBlock / G) * 4,
+                     s, k, X, xe, ym, ye, zpos, zneg, ze, u, v, w);
+  return hipGetLastError();
+}
+template <int C, int G>
+hipError_t run_decrypt(const Key& k, const uint32_t* ct, uint32_t* mag, signed char* neg, long long N,
+                       hipStream_t s) {
+  hipLaunchKernelGGL((k_decrypt<C, G>), dim3(grid_of(N, G)), dim3(kSlBlock), (size_t)(2 * C * G) * (kSlBlock / G) * 4, s, k, ct,
+                     mag, neg, N);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+// (L, C) pairs compiled: L = limbs of the modulus (2 ln for n^2 ops, ln for decryption)
+bool sliced_available(int L, int C) {
+  switch (L * 1000 + C) {
+    case 32016: case 64016: case 64032: case 128016: case 128032: case 256016: case 256032: return true;
+    default: return false;
+  }
+}
+
+#define SL_DISPATCH(L_, C_, EXPR)                            \
+  switch ((L_) * 1000 + (C_)) {                              \
+    case 32016: { constexpr int CC = 16, GG = 2; return EXPR; }  \
+    case 64016: { constexpr int CC = 16, GG = 4; return EXPR; }  \
+    case 64032: { constexpr int CC = 32, GG = 2; return EXPR; }  \
+    case 128016: { constexpr int CC = 16, GG = 8; return EXPR; } \
+    case 128032: { constexpr int CC = 32, GG = 4; return EXPR; } \
+    case 256016: { constexpr int CC = 16, GG = 16; return EXPR; } \
+    case 256032: { constexpr int CC = 32, GG = 8; return EXPR; } \
+    default: return hipErrorInvalidValue;                    \
+  }
+
+hipError_t sl_encrypt(const Key& k, int C, const long long* m, const uint32_t* hsa, uint32_t* out, long long N,
+                      uint64_t seed, long long ctr0, hipStream_t s) {
+  SL_DISPATCH(2 * k.d.ln, C, (run_encrypt<CC, GG>(k, m, hsa, out, N, seed, ctr0, s)))
+}
+hipError_t sl_fbpowm(const Key& k, int C, const uint32_t* a, uint32_t* out, long long N, uint64_t seed,
+                     long long ctr0, hipStream_t s) {
+  SL_DISPATCH(2 * k.d.ln, C, (run_fbpowm<CC, GG>(k, a, out, N, seed, ctr0, s)))
+}
+hipError_t sl_add(const Key& k, int C, const uint32_t* x, const uint32_t* y, uint32_t* out, long long N,
+                  hipStream_t s) {
+  SL_DISPATCH(2 * k.d.ln, C, (run_add<CC, GG>(k, x, y, out, N, s)))
+}
+hipError_t sl_powm(const Key& k, int C, const uint32_t* x, const uint32_t* e, int ew, uint32_t* out, long long N,
+                   hipStream_t s) {
+  SL_DISPATCH(2 * k.d.ln, C, (run_powm<CC, GG>(k, x, e, ew, out, N, s)))
+}
+hipError_t sl_matmul(const Key& k, int C, const uint32_t* X, const long long* xe, const long long* ym,
+                     const long long* ye, uint32_t* zpos, uint32_t* zneg, long long* ze, int u, int v, int w,
+                     hipStream_t s) {
+  SL_DISPATCH(2 * k.d.ln, C, (run_matmul<CC, GG>(k, X, xe, ym, ye, zpos, zneg, ze, u, v, w, s)))
+}
+hipError_t sl_decrypt(const Key& k, int C, const uint32_t* ct, uint32_t* mag, signed char* neg, long long N,
+                      hipStream_t s) {
+  SL_DISPATCH(k.d.ln, C, (run_decrypt<CC, GG>(k, ct, mag, neg, N, s)))
+}
+
+}  // namespace pl
+}  // namespace efl

@@ -21,7 +21,8 @@ import torch
 from efl import errors
 
 _LIB_DIR = os.path.dirname(os.path.realpath(__file__))
-LIB_PATH = os.path.join(_LIB_DIR, "libefl_hip.so")
+# EFL_HIP_LIB: path of a tuning build of the same library (Makefile `variant`); default in-tree
+LIB_PATH = os.environ.get("EFL_HIP_LIB") or os.path.join(_LIB_DIR, "libefl_hip.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(

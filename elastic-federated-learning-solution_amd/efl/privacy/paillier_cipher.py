@@ -54,9 +54,32 @@ for _name, _args in {
     "efl_pl_to_int64": [_vp, _i32, _vp, _vp, _i64, _vp],
     "efl_pl_invert": [_vp, _PK, _vp, _vp, _i64, _vp, _vp],
     "efl_pl_matmul": [_vp, _PK, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _vp],
+    "efl_pl_tune": [_i32, _i32, _i32],
 }.items():
     getattr(_lib, _name).argtypes = _args
     getattr(_lib, _name).restype = _i32
+
+
+def kernel_slicing(ln: int, decrypt: bool = False) -> int:
+    """Kernel family used for keys of `ln` 32-bit limbs: 0 = one lane per element, C = one number
+    spread over (2 ln or ln)/C lanes of C limbs (efl_pl_tune)."""
+    rc = _lib.efl_pl_tune(ln, int(bool(decrypt)), -1)
+    if rc < 0:
+        _efl_lib.check(rc)
+    return rc
+
+
+def set_kernel_slicing(ln: int, decrypt: bool, limbs_per_lane: int) -> int:
+    """Select the kernel family for keys of `ln` limbs; returns the previous choice."""
+    rc = _lib.efl_pl_tune(ln, int(bool(decrypt)), int(limbs_per_lane))
+    if rc < 0:
+        _efl_lib.check(rc)
+    return rc
+
+
+# kernel families compiled per key size (ln): n^2 ops, decryption
+SLICINGS = {16: ([0, 16], [0]), 32: ([0, 16, 32], [0, 16]), 64: ([0, 16, 32], [0, 16, 32]),
+            128: ([16, 32], [0, 16, 32])}
 
 _LIMB_CLASSES = (16, 32, 64, 128)
 MAX_TABLE_BITS = 1 << 40      # gmp_utils.h:20 FBPOWM_MAX_TABLE_MEM, compared against entries x bits

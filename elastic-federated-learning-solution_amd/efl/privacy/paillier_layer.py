@@ -228,6 +228,13 @@ class PaillierPassiveWeight(PaillierPassiveDense):
         return _ReceiverFn.apply(x_exponent, self.kernel, self)
 
 
+def _device_of(inputs):
+    """The receiver's kernel lives where its plaintext inputs are, else on the GPU the cipher runs on."""
+    if inputs is not None:
+        return inputs.device
+    return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+
+
 def _row(c, i):
     from efl.privacy.paillier_cipher import CipherTensor
     r, cols = c.shape
@@ -246,8 +253,7 @@ def dense_recv(inputs, keypair, communicator, prefix, recv_shape, units, activat
     layer = PaillierPassiveDense(keypair, communicator, prefix, units, kernel_initializer=kernel_initializer,
                                  seed=seed)
     x_exponent = communicator.recv(prefix + "_[x]_exponent", shape=recv_shape, dtype=torch.int64)
-    dev = inputs.device if inputs is not None else None
-    y = layer(x_exponent.to(dev) if dev is not None else x_exponent)
+    y = layer(x_exponent.to(_device_of(inputs)))
     if inputs is not None:
         lin = torch.nn.Linear(inputs.shape[-1], units, bias=use_bias).to(inputs.device)
         y = y + lin(inputs)
@@ -267,7 +273,7 @@ def weight_recv(inputs, keypair, communicator, prefix, units, kernel_initializer
     layer = PaillierPassiveWeight(keypair, communicator, prefix, units, kernel_initializer=kernel_initializer,
                                   seed=seed)
     x_exponent = communicator.recv(prefix + "_[x]_exponent", shape=(-1, units), dtype=torch.int64)
-    y = layer(x_exponent)
+    y = layer(x_exponent.to(_device_of(inputs)))
     if inputs is not None:
         y = y + inputs
     return y, layer.kernel

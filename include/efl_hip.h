@@ -161,7 +161,7 @@ typedef struct {
  * = (1 + |m| n)^(sign) * hsa mod n^2. hsa: [n][2*ln] limbs, or NULL for the reference's
  * hsa == "0" case: a fresh a of a_bits bits per element from Philox4x32-10(key = seed, counter =
  * counter_base + i) and hsa = hs^(a') through the fixed-base table (a' = a with every
- * group_size-bit group bit-reversed, as mpz_fbpowm does). n of up to 2048 bits.
+ * group_size-bit group bit-reversed, as mpz_fbpowm does). n of up to 4096 bits.
  */
 int efl_pl_encrypt(const void* key_block, const efl_pl_key* key, const int64_t* plaintext,
                    const uint32_t* hsa, uint32_t* ciphertext, int64_t n, uint64_t seed,
@@ -202,6 +202,13 @@ int efl_pl_matmul(const void* key_block, const efl_pl_key* key, const uint32_t* 
                   const int64_t* x_exponent, const int64_t* y_mantissa, const int64_t* y_exponent,
                   uint32_t* z_pos, uint32_t* z_neg, int64_t* z_exponent, int u, int v, int w,
                   void* stream);
+
+/* Kernel family for keys of ln limbs (16/32/64/128): decrypt = 0 selects the n^2 ops (encrypt,
+ * fbpowm, add, powm, matmul), 1 decryption. limbs_per_lane 0 = one lane per element (n^2 ops:
+ * ln <= 64 only), 16 or 32 = one number spread over L/limbs_per_lane lanes (L = 2 ln, or ln for
+ * decryption); -1 queries. Returns the previous choice, or a negative error code. Results are
+ * identical across families; only speed differs. */
+int efl_pl_tune(int ln, int decrypt, int limbs_per_lane);
 
 /* mpz_get_str(..., 16) of n numbers ([n][limbs_per_elem], optional sign bytes): first the text
  * lengths (efl_hex_lengths), then, given offsets = exclusive prefix sum (n + 1 entries), the

@@ -1,5 +1,8 @@
-"""GPU parity of Stage P (libefl_hip.so csrc/paillier.hip) against GMP-made known answers and the
-Python-int oracle. Bar: bit-exact ciphertext hex given hsa; exact decryption; exact fbpowm."""
+"""GPU parity of Stage P (libefl_hip.so csrc/paillier.hip, csrc/paillier_sliced.hip) against
+GMP-made known answers and the Python-int oracle. Bar: bit-exact ciphertext hex given hsa; exact
+decryption; exact fbpowm. Every kernel family (one lane per element, sliced over 16- or 32-limb
+lanes) is run on every key size it is compiled for."""
+import contextlib
 import json
 import os
 import random
@@ -16,8 +19,26 @@ pytestmark = pytest.mark.gpu
 
 with open(os.path.join(GOLDEN, "paillier_kat.json")) as f:
     KAT = json.load(f)
-ENC_KEYS = [k for k in KAT["keys"] if k["n_bytes"] <= 128]       # encrypt on GPU: n <= 2048 bits
+ENC_KEYS = [k for k in KAT["keys"] if k["n_bytes"] <= 128]
 ALL = KAT["keys"]
+# kernel families per ln (mirrors paillier_cipher.SLICINGS): (n^2 ops, decryption)
+SLICINGS = {16: ([0, 16], [0]), 32: ([0, 16, 32], [0, 16]), 64: ([0, 16, 32], [0, 16, 32]),
+            128: ([16, 32], [0, 16, 32])}
+
+
+def fams(keys, decrypt=False):
+    return [pytest.param(k, c, id=f"n{8 * k['n_bytes']}-C{c}")
+            for k in keys for c in SLICINGS[k["n_bytes"] // 4][1 if decrypt else 0]]
+
+
+@contextlib.contextmanager
+def family(ln, decrypt, c):
+    from efl.privacy import paillier_cipher as pc
+    prev = pc.set_kernel_slicing(ln, decrypt, c)
+    try:
+        yield
+    finally:
+        pc.set_kernel_slicing(ln, decrypt, prev)
 
 
 @pytest.fixture(scope="module")
@@ -38,55 +59,79 @@ def ids(k):
     return f"n{8 * k['n_bytes']}"
 
 
-@pytest.mark.parametrize("k", [k for k in ALL if k["n_bytes"] <= 256], ids=ids)
-def test_encrypt_given_hsa_kat(efl, k):
-    if k["n_bytes"] > 128:
-        pytest.skip("encrypt on the GPU: n up to 2048 bits")
+@pytest.mark.parametrize("k,c", fams(ALL))
+def test_encrypt_given_hsa_kat(efl, k, c):
     kp = keypair(efl, k)
     vs = k["vectors"]
     m = torch.tensor([v["m"] for v in vs], dtype=torch.int64, device="cuda")
-    ct = kp.encrypt(m, hsa=[v["hsa"] for v in vs])
+    with family(k["n_bytes"] // 4, False, c):
+        ct = kp.encrypt(m, hsa=[v["hsa"] for v in vs])
     assert ct.tensor.to_hex().strings() == [v["c"] for v in vs]
 
 
-@pytest.mark.parametrize("k", ALL, ids=ids)
-def test_decrypt_kat(efl, k):
+@pytest.mark.parametrize("k,c", fams(ALL, decrypt=True))
+def test_decrypt_kat(efl, k, c):
     kp = keypair(efl, k)
     vs = k["vectors"]
     hx = efl.HexTensor.from_strings([v["c"] for v in vs])
-    assert kp.decrypt(hx).strings() == [v["d"] for v in vs]
-    got = kp.decrypt(hx, dtype=torch.int64).cpu().tolist()
+    with family(k["n_bytes"] // 4, True, c):
+        assert kp.decrypt(hx).strings() == [v["d"] for v in vs]
+        got = kp.decrypt(hx, dtype=torch.int64).cpu().tolist()
     assert got == [v["m"] for v in vs]
 
 
-@pytest.mark.parametrize("k", ENC_KEYS, ids=ids)
-def test_fbpowm_kat(efl, k):
+@pytest.mark.parametrize("k,c", fams(ALL))
+def test_fbpowm_kat(efl, k, c):
     for g in sorted({v["g"] for v in k["vectors"]}):
         kp = keypair(efl, k, g=g)
         vs = [v for v in k["vectors"] if v["g"] == g]
-        out = kp.fbpowm(a=[int(v["a"], 16) for v in vs])
+        with family(k["n_bytes"] // 4, False, c):
+            out = kp.fbpowm(a=[int(v["a"], 16) for v in vs])
         assert out.to_hex().strings() == [v["hsa"] for v in vs]
 
 
-@pytest.mark.parametrize("k", ENC_KEYS, ids=ids)
-def test_homomorphic_ops_kat(efl, k):
+@pytest.mark.parametrize("k,c", fams(ALL))
+def test_homomorphic_ops_kat(efl, k, c):
     kp = keypair(efl, k)
     c0 = efl.HexTensor.from_strings([k["vectors"][5]["c"]])
     c1 = efl.HexTensor.from_strings([k["vectors"][6]["c"]])
-    assert kp.add(c0, c1).to_hex().strings() == [k["ops"]["add"]]
-    assert kp.mul_scalar(c0, 7).to_hex().strings() == [k["ops"]["mul_scalar_7"]]
-    assert kp.mul_exp2(c1, 5).to_hex().strings() == [k["ops"]["mul_exp2_5"]]
+    with family(k["n_bytes"] // 4, False, c):
+        assert kp.add(c0, c1).to_hex().strings() == [k["ops"]["add"]]
+        assert kp.mul_scalar(c0, 7).to_hex().strings() == [k["ops"]["mul_scalar_7"]]
+        assert kp.mul_exp2(c1, 5).to_hex().strings() == [k["ops"]["mul_exp2_5"]]
 
 
+@pytest.mark.parametrize("c", [16, 32])
+def test_round_trip_4096_fresh_randomness(efl, c):
+    """The reference's default key size (n of 4096 bits): fresh-randomness encryption through the
+    fixed-base table (sliced kernels) and CRT decryption, across many elements and both signs;
+    the ciphertexts equal the oracle's for the same Philox draws."""
+    k = ALL[3]
+    kp = keypair(efl, k, seed=99)
+    rng = np.random.default_rng(c)
+    m = torch.from_numpy(rng.integers(-2**63, 2**63 - 1, 300, dtype=np.int64))
+    m[:3] = torch.tensor([0, -1, 2**63 - 1])
+    with family(128, False, c), family(128, True, c):
+        ct = kp.encrypt(m, counter_base=5)
+        assert torch.equal(kp.decrypt(ct, dtype=torch.int64).cpu(), m)
+    okp = P.Keypair(int(k["n"], 16), int(k["hs"], 16), k["a_bits"] // 8, 1, int(k["p"], 16), int(k["q"], 16))
+    got = ct.tensor.to_hex().strings()
+    for i in (0, 1, 2, 77, 299):
+        a = philox.draw_a(99, 5 + i, k["a_bits"])
+        assert got[i] == P.hx(P.encrypt(okp, int(m[i]), P.fbpowm(okp.hs, okp.n2, a, 1))), i
+
+
+@pytest.mark.parametrize("c", [0, 16])
 @pytest.mark.parametrize("g", [1, 3])
-def test_encrypt_random_a_is_philox_stream(efl, g):
+def test_encrypt_random_a_is_philox_stream(efl, g, c):
     """hsa == 0 path: a = Philox(seed, counter_base + i); c == oracle encrypt with hs^(a')."""
     k = ENC_KEYS[0]
     kp = keypair(efl, k, g=g, seed=0xC0FFEE)
     okp = P.Keypair(int(k["n"], 16), int(k["hs"], 16), k["a_bits"] // 8, g, int(k["p"], 16), int(k["q"], 16))
     rng = random.Random(g)
     ms = [rng.randrange(-2**63, 2**63) for _ in range(70)]
-    ct = kp.encrypt(torch.tensor(ms), counter_base=1000)
+    with family(16, False, c):
+        ct = kp.encrypt(torch.tensor(ms), counter_base=1000)
     got = ct.tensor.to_hex().strings()
     for i, m in enumerate(ms):
         a = philox.draw_a(0xC0FFEE, 1000 + i, k["a_bits"])
@@ -163,9 +208,15 @@ def test_fixed_point_add_like_reference_test(efl):
     assert np.array_equal(c2.cpu().numpy().reshape(-1).view(np.uint32), want.view(np.uint32))
 
 
-def test_invert_and_negative_scalars(efl):
+@pytest.mark.parametrize("c", [0, 16, 32])
+def test_invert_and_negative_scalars(efl, c):
     k = ENC_KEYS[1]
     kp = keypair(efl, k)
+    with family(32, False, c):
+        _invert_and_negative_scalars(efl, k, kp)
+
+
+def _invert_and_negative_scalars(efl, k, kp):
     okp = P.Keypair(int(k["n"], 16), int(k["hs"], 16), k["a_bits"] // 8, 1, int(k["p"], 16), int(k["q"], 16))
     cs = [int(v["c"], 16) for v in k["vectors"][:12]]
     hx = efl.HexTensor.from_ints(cs)
@@ -177,7 +228,13 @@ def test_invert_and_negative_scalars(efl):
         kp.invert(efl.HexTensor.from_ints([okp.n]))         # gcd(n, n^2) != 1
 
 
-def test_matmul_vs_oracle(efl):
+@pytest.mark.parametrize("c", [0, 16])
+def test_matmul_vs_oracle(efl, c):
+    with family(16, False, c):
+        _matmul_vs_oracle(efl)
+
+
+def _matmul_vs_oracle(efl):
     k = ENC_KEYS[0]
     kp = keypair(efl, k)
     okp = P.Keypair(int(k["n"], 16), int(k["hs"], 16), k["a_bits"] // 8, 1, int(k["p"], 16), int(k["q"], 16))
