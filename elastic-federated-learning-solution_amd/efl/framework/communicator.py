@@ -291,6 +291,7 @@ class Communicator(object):
 
     def _on_send_message(self, request, context):
         name, step, tensor = wire.parse_message_request(request)
+        log.debug("%s: arrived %s step %d", self._federal_role, name, step)
         p = _Parked(step, tensor)
         with self._lock:
             w = self._waiters.pop((name, step), None)
@@ -346,6 +347,7 @@ class Communicator(object):
 
     def _recv_raw(self, name, dtype=None):
         step = self.step
+        log.debug("%s: waiting %s step %d", self._federal_role, name, step)
         deadline = time.monotonic() + self._timeout
         with self._lock:
             p, w = self._take(name, step)

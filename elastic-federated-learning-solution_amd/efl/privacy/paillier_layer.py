@@ -173,12 +173,12 @@ class PaillierPassiveDense(_LayerBase):
         if x_exponent.dim() > 2:
             raise ValueError("PaillierDense hasn't support broadcasting yet.")
         if self.kernel is None:
-            w = torch.empty(x_exponent.shape[-1], self.units, device=x_exponent.device)
+            w = torch.empty(x_exponent.shape[-1], self.units)          # host draw: seeded generator
             if self._init is None:
                 torch.nn.init.xavier_uniform_(w, generator=self.generator)
             else:
                 self._init(w)
-            self.kernel = torch.nn.Parameter(w)
+            self.kernel = torch.nn.Parameter(w.to(x_exponent.device))
         return _ReceiverFn.apply(x_exponent, self.kernel, self)
 
 

@@ -1,8 +1,13 @@
 """GPU: the two-party Paillier Dense / Weight layers (paillier_layer.py protocol) end to end over
 two communicators on loopback, with the key exchanged by efl.paillier.Hook. Checks the plaintext
 meaning of every exchanged quantity against torch fp32 (tolerance from the reference's own
-decrease_precision fixed-point encoding of W and dy: 13 dropped mantissa bits, rtol 1e-2)."""
-import threading
+decrease_precision fixed-point encoding of W and dy: 13 dropped mantissa bits, rtol 1e-2).
+
+Each party runs in its own process, as in a federated deployment: the protocol blocks inside
+backward() on messages the peer sends from ITS backward(), and torch runs every backward() of a
+process on one autograd thread per device, so two parties sharing a process would wait on each
+other forever."""
+import multiprocessing as mp
 
 import pytest
 import torch
@@ -11,75 +16,78 @@ from test_communicator import free_port
 
 pytestmark = pytest.mark.gpu
 
+B, F = 8, 6
 
-def run_pair(sender_fn, receiver_fn):
-    import efl
-    pl, pf = free_port(), free_port()
-    comms = {}
-    results, errs = {}, []
 
-    def party(role, fn, my, peer):
-        try:
-            c = efl.Communicator(role, 0, 1, f"127.0.0.1:{peer}", f"127.0.0.1:{my}",
-                                 default_timeout_milliseconds=120000, connect_retry_seconds=0.1)
-            c.initialize()
-            comms[role] = c
-            results[role] = fn(c)
-        except Exception as e:  # pragma: no cover
-            errs.append((role, e))
-            raise
-    ts = [threading.Thread(target=party, args=("leader", receiver_fn, pl, pf)),
-          threading.Thread(target=party, args=("follower", sender_fn, pf, pl))]
-    for t in ts:
-        t.start()
-    for t in ts:
-        t.join(300)
-    for c in comms.values():
+def data(kind):
+    g = torch.Generator().manual_seed(0)
+    units = 3 if kind == "dense" else F
+    x = torch.randn(B, F, generator=g)
+    dy_r = torch.randn(B, units, generator=g)
+    dy_s = torch.randn(B, units, generator=g)
+    return units, x, dy_r, dy_s
+
+
+def party(role, kind, my, peer, q):
+    try:
+        import efl
+        Role = efl.privacy.Role
+        units, x, dy_r, dy_s = data(kind)
+        c = efl.Communicator(role, 0, 1, f"127.0.0.1:{peer}", f"127.0.0.1:{my}",
+                             default_timeout_milliseconds=120000, connect_retry_seconds=0.1)
+        c.initialize()
+        kp = efl.paillier.Keypair()
+        if role == "follower":   # sender: owns the key, holds x
+            efl.paillier.Hook(kp, c, Role.SENDER, "k", n_bytes=64).after_create_session()
+            xi = x.cuda().requires_grad_(True)
+            fn = efl.paillier.sender.dense if kind == "dense" else efl.paillier.sender.weight
+            out, w = fn(xi, kp, c, "l1", units, seed=1)
+            out.backward(dy_s.cuda())
+            res = (out.detach().cpu(), xi.grad.cpu(), w.grad.cpu())
+        else:                    # receiver: holds W
+            efl.paillier.Hook(kp, c, Role.RECEIVER, "k", n_bytes=64).after_create_session()
+            if kind == "dense":
+                y, w = efl.paillier.recver.dense(None, kp, c, "l1", (B, F), units, seed=2)
+            else:
+                gw = torch.Generator().manual_seed(3)
+                y, w = efl.paillier.recver.weight(None, kp, c, "l1", units, seed=2,
+                                                  kernel_initializer=lambda t: t.copy_(torch.rand(t.shape, generator=gw) - 0.5))
+            y.backward(dy_r.cuda())
+            res = (y.detach().cpu(), w.detach().cpu(), w.grad.cpu())
         c.shutdown()
-    assert not errs, errs
-    return results
+        q.put((role, res, None))
+    except BaseException as e:  # pragma: no cover - reported to the parent
+        q.put((role, None, repr(e)))
 
 
 @pytest.mark.parametrize("kind", ["dense", "weight"])
 def test_paillier_layer_two_party(kind):
-    import efl
-    g = torch.Generator().manual_seed(0)
-    B, F = 8, 6
-    units = 3 if kind == "dense" else F
-    x = torch.randn(B, F, generator=g).cuda()
-    dy_r = torch.randn(B, units, generator=g).cuda()
-    dy_s = torch.randn(B, units, generator=g).cuda()
-    Role = efl.privacy.Role
-
-    def sender(c):
-        kp = efl.paillier.Keypair()
-        efl.paillier.Hook(kp, c, Role.SENDER, "k", n_bytes=64).after_create_session()
-        xi = x.clone().requires_grad_(True)
-        if kind == "dense":
-            out, w = efl.paillier.sender.dense(xi, kp, c, "l1", units, seed=1)
-        else:
-            out, w = efl.paillier.sender.weight(xi, kp, c, "l1", units, seed=1)
-        out.backward(dy_s)
-        return out.detach(), xi.grad, w.grad
-
-    def receiver(c):
-        kp = efl.paillier.Keypair()
-        efl.paillier.Hook(kp, c, Role.RECEIVER, "k", n_bytes=64).after_create_session()
-        if kind == "dense":
-            y, w = efl.paillier.recver.dense(None, kp, c, "l1", (B, F), units, seed=2)
-        else:
-            y, w = efl.paillier.recver.weight(None, kp, c, "l1", units, seed=2)
-        y.backward(dy_r)
-        return y.detach(), w.detach(), w.grad
-
-    res = run_pair(sender, receiver)
-    y, W, dW = res["leader"]
-    out, dx, dws = res["follower"]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pl, pf = free_port(), free_port()
+    procs = [ctx.Process(target=party, args=("leader", kind, pl, pf, q)),
+             ctx.Process(target=party, args=("follower", kind, pf, pl, q))]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in procs:
+            role, res, err = q.get(timeout=400)
+            assert err is None, (role, err)
+            results[role] = res
+    finally:
+        for p in procs:
+            p.join(30)
+            if p.is_alive():
+                p.kill()
+    y, W, dW = results["leader"]
+    out, dx, dws = results["follower"]
+    units, x, dy_r, _ = data(kind)
     if kind == "dense":
         want_y, want_dw, want_dx = x @ W, x.t() @ dy_r, dy_r @ W.t()
     else:
         want_y, want_dw, want_dx = x * W, (x * dy_r).sum(0), dy_r * W
-    assert torch.allclose(y.cuda(), want_y, rtol=1e-2, atol=1e-2)
-    assert torch.allclose(dW.cuda(), want_dw, rtol=1e-2, atol=1e-2)
-    assert torch.allclose(dx.cuda(), want_dx, rtol=1e-2, atol=1e-2)
-    assert dws is not None and torch.isfinite(dws).all()      # -nf noise for the sender's zero kernel
+    assert torch.allclose(y, want_y, rtol=1e-2, atol=1e-2)
+    assert torch.allclose(dW, want_dw, rtol=1e-2, atol=1e-2)
+    assert torch.allclose(dx, want_dx, rtol=1e-2, atol=1e-2)
+    assert torch.isfinite(dws).all()      # -nf noise for the sender's zero kernel

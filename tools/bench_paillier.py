@@ -1,9 +1,14 @@
 #!/usr/bin/env python3
 """Stage P throughput on one MI355X (BASELINE.md §2 'Stage P'): elements/s for encrypt given hsa,
-encrypt with fresh randomness (fixed-base table), and CRT decrypt, at N = 262,144 and the MNIST
-shape [256, 392], for the key sizes the GPU path supports. One JSON line per (key, op)."""
+encrypt with fresh randomness (fixed-base table), and CRT decrypt, for every key size and every
+kernel family compiled for it (efl_pl_tune: 0 = one lane per element, 16/32 = sliced).
+One JSON line per (key, N, family). Kernel-only timing with HIP events on the launch stream.
+
+Env: PL_KEYS "n_bytes:group_size,..." (default 64:1,128:1,128:10,256:1,256:10,512:1),
+     PL_N     elements per launch for n < 4096 bits (default 262144), PL_N4096 (default 65536)."""
 import json
 import os
+import random
 import sys
 import time
 
@@ -17,21 +22,25 @@ from efl.privacy import paillier_cipher as pc  # noqa: E402
 
 dev = efl.lib.require_gpu()
 lib = efl.lib.raw()
-sizes = [int(s) for s in os.environ.get("PL_SIZES", "262144,100352").split(",")]
-keys = [(int(b), int(g)) for b, g in (x.split(":") for x in os.environ.get("PL_KEYS", "64:1,128:1,128:10,256:1").split(","))]
+keys = [(int(b), int(g)) for b, g in (x.split(":") for x in
+                                       os.environ.get("PL_KEYS", "64:1,128:1,128:10,256:1,256:10,512:1").split(","))]
+N_SMALL = int(os.environ.get("PL_N", "262144"))
+N_4096 = int(os.environ.get("PL_N4096", "65536"))
 
 
-def timed(fn, reps=3):
-    fn()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
+def timed(fn, reps=1):
+    fn()                                   # warmup (and first-launch code object load)
+    s = torch.cuda.current_stream()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(s)
     for _ in range(reps):
         fn()
-    torch.cuda.synchronize()
-    return (time.perf_counter() - t0) / reps
+    b.record(s)
+    b.synchronize()
+    return a.elapsed_time(b) / 1e3 / reps
 
 
-import random  # noqa: E402
+# KAT-free keys: deterministic Miller-Rabin keys per size (host keygen is not on the hot path)
 for n_bytes, g in keys:
     t0 = time.perf_counter()
     n, hs, p, q = pc.generate_keypair_ints(n_bytes, 24, random.Random(n_bytes))
@@ -39,25 +48,36 @@ for n_bytes, g in keys:
     kp.set_keys_ints(n, hs, n_bytes // 2, g, p, q, n_bytes)
     setup = time.perf_counter() - t0
     k = kp.key
-    for N in sizes:
-        m = torch.randint(-2**40, 2**40, (N,), dtype=torch.int64, device=dev)
-        out = torch.empty((N, k.lc), dtype=torch.int32, device=dev)
-        hsa = kp.fbpowm(n=N).limbs
-        s = torch.cuda.current_stream().cuda_stream
-        res = {"n_bits": 8 * n_bytes, "group_size": g, "N": N, "key_setup_s": round(setup, 2)}
-        if k.ln <= 64:
+    N = N_4096 if k.ln >= 128 else N_SMALL
+    m = torch.randint(-2**40, 2**40, (N,), dtype=torch.int64, device=dev)
+    out = torch.empty((N, k.lc), dtype=torch.int32, device=dev)
+    mag = torch.empty((N, k.ln), dtype=torch.int32, device=dev)
+    neg = torch.empty(N, dtype=torch.int8, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    fams_enc, fams_dec = pc.SLICINGS[k.ln]
+    base_enc, base_dec = pc.kernel_slicing(k.ln, False), pc.kernel_slicing(k.ln, True)
+    hsa = kp.fbpowm(n=N).limbs
+    for c in fams_enc:
+        pc.set_kernel_slicing(k.ln, False, c)
+        res = {"n_bits": 8 * n_bytes, "group_size": g, "N": N, "op_family": c, "key_setup_s": round(setup, 2)}
+        if g == 1:
             t = timed(lambda: efl.lib.check(lib.efl_pl_encrypt(*k.args(), m.data_ptr(), hsa.data_ptr(),
-                                                               out.data_ptr(), N, 7, 0, s)))
+                                                               out.data_ptr(), N, 7, 0, s)), reps=3)
             res["encrypt_given_hsa_per_s"] = round(N / t)
-            t = timed(lambda: efl.lib.check(lib.efl_pl_encrypt(*k.args(), m.data_ptr(), None, out.data_ptr(),
-                                                               N, 7, 0, s)), reps=1)
-            res["encrypt_fresh_per_s"] = round(N / t)
-        ct = out
-        mag = torch.empty((N, k.ln), dtype=torch.int32, device=dev)
-        neg = torch.empty(N, dtype=torch.int8, device=dev)
-        t = timed(lambda: efl.lib.check(lib.efl_pl_decrypt(*k.args(), ct.data_ptr(), mag.data_ptr(), neg.data_ptr(),
-                                                           N, s)), reps=1)
-        res["decrypt_per_s"] = round(N / t)
-        dec = kp.decrypt(pc.CipherTensor(ct[:64], (64,), k), dtype=torch.int64)
-        res["round_trip_ok"] = bool(torch.equal(dec, m[:64]))
+        t = timed(lambda: efl.lib.check(lib.efl_pl_encrypt(*k.args(), m.data_ptr(), None, out.data_ptr(),
+                                                           N, 7, 0, s)))
+        res["encrypt_fresh_per_s"] = round(N / t)
         print(json.dumps(res), flush=True)
+    pc.set_kernel_slicing(k.ln, False, base_enc)
+    ct = out
+    for c in fams_dec:
+        pc.set_kernel_slicing(k.ln, True, c)
+        t = timed(lambda: efl.lib.check(lib.efl_pl_decrypt(*k.args(), ct.data_ptr(), mag.data_ptr(),
+                                                           neg.data_ptr(), N, s)))
+        dec = kp.decrypt(pc.CipherTensor(ct[:256], (256,), k), dtype=torch.int64)
+        print(json.dumps({"n_bits": 8 * n_bytes, "group_size": g, "N": N, "dec_family": c,
+                          "decrypt_per_s": round(N / t), "round_trip_ok": bool(torch.equal(dec, m[:256]))}),
+              flush=True)
+    pc.set_kernel_slicing(k.ln, True, base_dec)
+    del out, mag, neg, hsa
+    torch.cuda.empty_cache()
