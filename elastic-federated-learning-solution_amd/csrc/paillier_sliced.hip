@@ -510,6 +510,7 @@ hipError_t run_decrypt(const Key& k, const uint32_t* ct, uint32_t* mag, signed c
 // (L, C) pairs compiled: L = limbs of the modulus (2 ln for n^2 ops, ln for decryption)
 bool sliced_available(int L, int C) {
   switch (L * 1000 + C) {
+    case 16008: case 32008: case 64008: case 128008: case 256008:
     case 32016: case 64016: case 64032: case 128016: case 128032: case 256016: case 256032: return true;
     default: return false;
   }
@@ -517,6 +518,11 @@ bool sliced_available(int L, int C) {
 
 #define SL_DISPATCH(L_, C_, EXPR)                            \
   switch ((L_) * 1000 + (C_)) {                              \
+    case 16008: { constexpr int CC = 8, GG = 2; return EXPR; }   \
+    case 32008: { constexpr int CC = 8, GG = 4; return EXPR; }   \
+    case 64008: { constexpr int CC = 8, GG = 8; return EXPR; }   \
+    case 128008: { constexpr int CC = 8, GG = 16; return EXPR; } \
+    case 256008: { constexpr int CC = 8, GG = 32; return EXPR; } \
     case 32016: { constexpr int CC = 16, GG = 2; return EXPR; }  \
     case 64016: { constexpr int CC = 16, GG = 4; return EXPR; }  \
     case 64032: { constexpr int CC = 32, GG = 2; return EXPR; }  \

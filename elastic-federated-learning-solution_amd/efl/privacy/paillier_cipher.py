@@ -78,8 +78,8 @@ def set_kernel_slicing(ln: int, decrypt: bool, limbs_per_lane: int) -> int:
 
 
 # kernel families compiled per key size (ln): n^2 ops, decryption
-SLICINGS = {16: ([0, 16], [0]), 32: ([0, 16, 32], [0, 16]), 64: ([0, 16, 32], [0, 16, 32]),
-            128: ([16, 32], [0, 16, 32])}
+SLICINGS = {16: ([0, 8, 16], [0, 8]), 32: ([0, 8, 16, 32], [0, 8, 16]), 64: ([0, 8, 16, 32], [0, 8, 16, 32]),
+            128: ([8, 16, 32], [0, 8, 16, 32])}
 
 _LIMB_CLASSES = (16, 32, 64, 128)
 MAX_TABLE_BITS = 1 << 40      # gmp_utils.h:20 FBPOWM_MAX_TABLE_MEM, compared against entries x bits
