@@ -95,6 +95,22 @@ __device__ __forceinline__ float d2f(unsigned long long dbits, bool ftz) {
   return (float)__longlong_as_double((long long)dbits);
 }
 
+// Fast path of get_d_bits. For |M| < 2^53 and E >= -1022 the value M * 2^E is exact in a double
+// (normal, zero, or >= 2^1024 where both GMP and the hardware give +-inf), so GMP's truncation
+// never acts and mpf_get_d == ldexp((double)M, E) bit for bit: an exact int64 -> f64 convert and
+// one v_ldexp_f64 instead of the bit-by-bit rebuild. Every mantissa ConvertToFixedPoint<float>
+// produces takes it (|M| < 2^24, E >= -277); anything else falls back to dec_bits.
+__device__ __forceinline__ bool dec_fast_ok(long long M, long long E) {
+  return (unsigned long long)M + (1ull << 53) < (1ull << 54) && E >= -1022;
+}
+__device__ __forceinline__ unsigned long long dec_fast_bits(long long M, long long E) {
+  const int e = E > 4096 ? 4096 : (int)E;   // anything past 2^1024 is inf already
+  return (unsigned long long)__double_as_longlong(ldexp((double)M, e));
+}
+__device__ __forceinline__ unsigned long long dec_any_bits(long long M, long long E) {
+  return dec_fast_ok(M, E) ? dec_fast_bits(M, E) : dec_bits(M, E);
+}
+
 // ------------------------------------------------------------------------------------------
 // memory helpers (NT bit 0: nontemporal loads, bit 1: nontemporal stores)
 // ------------------------------------------------------------------------------------------
@@ -213,11 +229,11 @@ struct DecF32Pair {
   }
   template <int NT> __device__ static void apply(const Args& a, long long u, In v) {
     const bool ftz = a.flag & EFL_FXP_FTZ;
-    f2 r{d2f(dec_bits(v.m.x, v.e.x), ftz), d2f(dec_bits(v.m.y, v.e.y), ftz)};
+    f2 r{d2f(dec_any_bits(v.m.x, v.e.x), ftz), d2f(dec_any_bits(v.m.y, v.e.y), ftz)};
     st<NT>((f2*)a.y + u, r);
   }
   __device__ static void scalar(const Args& a, long long i) {
-    ((float*)a.y)[i] = d2f(dec_bits(a.M[i], a.E[i]), a.flag & EFL_FXP_FTZ);
+    ((float*)a.y)[i] = d2f(dec_any_bits(a.M[i], a.E[i]), a.flag & EFL_FXP_FTZ);
   }
 };
 
@@ -232,8 +248,8 @@ struct DecF32Quad {
   }
   template <int NT> __device__ static void apply(const Args& a, long long u, In v) {
     const bool ftz = a.flag & EFL_FXP_FTZ;
-    f4 r{d2f(dec_bits(v.m0.x, v.e0.x), ftz), d2f(dec_bits(v.m0.y, v.e0.y), ftz),
-         d2f(dec_bits(v.m1.x, v.e1.x), ftz), d2f(dec_bits(v.m1.y, v.e1.y), ftz)};
+    f4 r{d2f(dec_any_bits(v.m0.x, v.e0.x), ftz), d2f(dec_any_bits(v.m0.y, v.e0.y), ftz),
+         d2f(dec_any_bits(v.m1.x, v.e1.x), ftz), d2f(dec_any_bits(v.m1.y, v.e1.y), ftz)};
     st<NT>((f4*)a.y + u, r);
   }
   __device__ static void scalar(const Args& a, long long i) { DecF32Pair::scalar(a, i); }
@@ -247,11 +263,11 @@ struct DecF64Pair {
     return In{ld<NT>((const ll2*)a.M + u), ld<NT>((const ll2*)a.E + u)};
   }
   template <int NT> __device__ static void apply(const Args& a, long long u, In v) {
-    ll2 r{(long long)dec_bits(v.m.x, v.e.x), (long long)dec_bits(v.m.y, v.e.y)};
+    ll2 r{(long long)dec_any_bits(v.m.x, v.e.x), (long long)dec_any_bits(v.m.y, v.e.y)};
     st<NT>((ll2*)a.y + u, r);
   }
   __device__ static void scalar(const Args& a, long long i) {
-    ((unsigned long long*)a.y)[i] = dec_bits(a.M[i], a.E[i]);
+    ((unsigned long long*)a.y)[i] = dec_any_bits(a.M[i], a.E[i]);
   }
 };
 
@@ -271,6 +287,9 @@ __global__ __launch_bounds__(B) void k_stream(typename Op::Args a, long long nun
     if (base + tile <= nunits) {
 #pragma unroll
       for (int k = 0; k < K; ++k) v[k] = Op::template load<NT>(a, base + k * B + threadIdx.x);
+      // keep every load of the tile issued before any of the transform: without this fence the
+      // scheduler may start converting the first stream and wait for it before issuing the second
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int k = 0; k < K; ++k) Op::template apply<NT>(a, base + k * B + threadIdx.x, v[k]);
     } else {
@@ -297,11 +316,12 @@ __global__ __launch_bounds__(kBlock) void k_scalar(typename Op::Args a, long lon
 }
 
 // Batched: blockIdx.y = tensor, blockIdx.x = tile of that tensor (one launch for `count`
-// tensors; BASELINE config 3). Arrays of pointers / sizes live in device memory.
-template <class Op, int K, int NT>
-__global__ __launch_bounds__(kBlock) void k_batched(const void* const* src, void* const* dst0,
-                                                    void* const* dst1, const long long* ns,
-                                                    int flag, long long tile_base) {
+// tensors; BASELINE config 3). Arrays of pointers / sizes live in device memory. Same tile shape
+// as k_stream (B lanes x K units, every load of a full tile issued before the transform).
+template <class Op, int B, int K, int NT>
+__global__ __launch_bounds__(B) void k_batched(const void* const* src, void* const* dst0,
+                                               void* const* dst1, const long long* ns,
+                                               int flag, long long tile_base) {
   const long long t = tile_base + blockIdx.y;
   const long long n = ns[t];
   typename Op::Args a;
@@ -310,18 +330,32 @@ __global__ __launch_bounds__(kBlock) void k_batched(const void* const* src, void
   } else {
     a = DecArgs{(const long long*)src[t], (const long long*)dst0[t], dst1[t], flag};
   }
-  const long long tile = (long long)kBlock * K * Op::kElems;
+  const long long tile = (long long)B * K * Op::kElems;
   const long long e0 = (long long)blockIdx.x * tile;
   if (e0 >= n) return;
   // 16-B alignment of this tensor's streams decides vector vs element path (uniform branch).
   const bool vec = aligned(src[t], 16) && aligned(dst0[t], 16) && aligned(dst1[t], 16);
   const long long nunits = n / Op::kElems;
-  const long long u0 = (long long)blockIdx.x * kBlock * K;
+  const long long u0 = (long long)blockIdx.x * B * K;
   if (vec) {
+    typename Op::In v[K];
+    if (u0 + (long long)B * K <= nunits) {
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const long long u = u0 + k * kBlock + threadIdx.x;
-      if (u < nunits) Op::template apply<NT>(a, u, Op::template load<NT>(a, u));
+      for (int k = 0; k < K; ++k) v[k] = Op::template load<NT>(a, u0 + k * B + threadIdx.x);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int k = 0; k < K; ++k) Op::template apply<NT>(a, u0 + k * B + threadIdx.x, v[k]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const long long u = u0 + k * B + threadIdx.x;
+        if (u < nunits) v[k] = Op::template load<NT>(a, u);
+      }
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const long long u = u0 + k * B + threadIdx.x;
+        if (u < nunits) Op::template apply<NT>(a, u, v[k]);
+      }
     }
     // ragged tail (< kElems elements) of this tensor, handled by the tile that owns it
     const long long tail0 = nunits * Op::kElems;
@@ -329,7 +363,7 @@ __global__ __launch_bounds__(kBlock) void k_batched(const void* const* src, void
       if (threadIdx.x < n - tail0) Op::scalar(a, tail0 + threadIdx.x);
     }
   } else {
-    for (long long i = e0 + threadIdx.x; i < n && i < e0 + tile; i += kBlock) Op::scalar(a, i);
+    for (long long i = e0 + threadIdx.x; i < n && i < e0 + tile; i += B) Op::scalar(a, i);
   }
 }
 
@@ -602,19 +636,22 @@ EFL_API int efl_fxp_decode_hex(const char* chars, const int64_t* offsets, const 
 }
 
 namespace {
-constexpr int kBatchK = 4;
+// batched tile: 256 lanes x 4 pairs (2048 elements), nontemporal loads: fewer, longer workgroups
+// amortise the per-workgroup pointer-table reads (measured faster than the k_stream shape here)
+constexpr int kBatchB = 256, kBatchK = 4;
 constexpr long long kMaxGridY = 65535;
 
 template <class Op, int NT>
 hipError_t launch_batched(const void* const* src, void* const* d0, void* const* d1,
                           const long long* ns, long long count, long long max_n, int flag,
                           hipStream_t s) {
-  const long long tile = (long long)kBlock * kBatchK * Op::kElems;
+  const long long tile = (long long)kBatchB * kBatchK * Op::kElems;
   const long long gx = (max_n + tile - 1) / tile;
   if (gx == 0 || count == 0) return hipSuccess;
+  if (gx > 0x7FFFFFFFll) return hipErrorInvalidValue;
   for (long long b = 0; b < count; b += kMaxGridY) {
     const long long gy = count - b < kMaxGridY ? count - b : kMaxGridY;
-    hipLaunchKernelGGL((k_batched<Op, kBatchK, NT>), dim3((unsigned)gx, (unsigned)gy), dim3(kBlock), 0, s,
+    hipLaunchKernelGGL((k_batched<Op, kBatchB, kBatchK, NT>), dim3((unsigned)gx, (unsigned)gy), dim3(kBatchB), 0, s,
                        src, d0, d1, ns, flag, b);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

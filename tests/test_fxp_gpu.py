@@ -88,6 +88,25 @@ def test_decode_i64_f64_golden(efl):
     assert np.array_equal(bits64(y), G["dec_f64"])
 
 
+def test_decode_fast_path_boundaries(efl):
+    """The decode kernels take an exact ldexp path for |M| < 2^53 and E >= -1022 and GMP's
+    bit-by-bit truncation otherwise: every pair straddling that boundary, in every vector lane
+    position (odd-sized batches reach the scalar tail too), against the GMP-pinned oracle."""
+    ms = [0, 1, -1, 3, (1 << 53) - 1, -((1 << 53) - 1), 1 << 53, -(1 << 53), (1 << 53) + 1,
+          -((1 << 53) + 1), (1 << 62) + 12345, -(1 << 63), (1 << 63) - 1, 0x00FFFFFF, -0x00FFFFFF]
+    es = [-1023, -1022, -1021, -1074, -1075, -1200, -150, -149, 0, 971, 972, 1000, 4096, 4097,
+          1 << 40, -(1 << 40), (1 << 62), -(1 << 62)]
+    M = np.array([m for m in ms for _ in es], np.int64)
+    E = np.array([e for _ in ms for e in es], np.int64)
+    for sl in (slice(None), slice(1, None), slice(0, -3)):
+        m, e = M[sl], E[sl]
+        for ftz in (0, 1):
+            y = efl.lib.ops.fixed_point_to_float_point(dev(m), dev(e), "float32", flush_denormal=bool(ftz))
+            assert np.array_equal(bits32(y), fxp.gmp_decode(m, e, np.float32, bool(ftz)).view(np.uint32))
+        y = efl.lib.ops.fixed_point_to_float_point(dev(m), dev(e), torch.float64)
+        assert np.array_equal(bits64(y), fxp.gmp_decode(m, e, np.float64).view(np.uint64))
+
+
 def _hex():
     b, o = H["buf"].tobytes(), H["offs"]
     return [b[o[i]:o[i + 1]] for i in range(o.size - 1)]

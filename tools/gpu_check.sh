@@ -11,6 +11,11 @@ run_tests() { timeout -k 10 900 python -m pytest tests -m gpu -x -q > $O/pytest_
 run_smoke() { timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1; }
 run_bench() { timeout -k 10 300 python bench.py --steps 50 --warmup 5 > $O/bench.json 2> $O/bench.err && timeout -k 10 300 python tools/bench_batched.py > $O/bench_batched.json 2> $O/bench_batched.err && timeout -k 10 600 python tools/bench_e2e.py > $O/bench_e2e.json 2> $O/bench_e2e.err; }
 run_sweep() { timeout -k 10 300 python tools/sweep_fxp.py > $O/sweep.jsonl 2> $O/sweep.err; }
+# traffic-mix HBM ceilings and VALU issue rates (tools/*.hip, built on the CPU side beforehand)
+run_probes() {
+  timeout -k 10 120 tools/stream_probe > $O/stream_probe.json 2> $O/stream_probe.err &&
+  timeout -k 10 120 tools/valu_probe > $O/valu_probe.jsonl 2> $O/valu_probe.err
+}
 run_prof() {
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_trace -o run --output-format csv \
       -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > $O/prof_trace.log 2>&1 &&
@@ -21,6 +26,8 @@ run_prof() {
 }
 case $STAGE in
   all) run_tests && run_smoke && run_bench && run_sweep && run_prof ;;
+  round) run_tests && run_smoke && run_probes && run_bench && run_prof ;;
+  probes) run_probes ;;
   tests) run_tests ;;
   bench) run_bench && run_sweep ;;
   prof) run_prof ;;

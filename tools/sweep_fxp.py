@@ -28,8 +28,11 @@ DEFAULT = {d: {f: lib.efl_fxp_tune(2 * f + d, v) for f, v in ((0, 0), (1, 1), (2
 for d in (0, 1):
     for f, v in DEFAULT[d].items():
         lib.efl_fxp_tune(2 * f + d, v)
+LAYOUTS = [int(v) for v in os.environ.get("SWEEP_LAYOUTS", "0,1").split(",")]
+NTS = [int(v) for v in os.environ.get("SWEEP_NT", "0,1,2,3").split(",")]
+DIRS = [{"encode": 0, "decode": 1}[d] for d in os.environ.get("SWEEP_DIRS", "encode,decode").split(",")]
 shapes = [dict(layout=l, K=k, nt=t, block=b) for l, k, t, b in
-          itertools.product((0, 1), (1, 2), (0, 1, 2, 3), (128, 256, 512))]
+          itertools.product(LAYOUTS, (1, 2), NTS, (128, 256, 512))]
 rounds = int(os.environ.get("SWEEP_ROUNDS", "4"))
 reps = 3
 
@@ -45,9 +48,9 @@ def restore(d):
 
 
 ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-res = {(d, i): [] for d in (0, 1) for i in range(len(shapes))}
+res = {(d, i): [] for d in DIRS for i in range(len(shapes))}
 for r in range(rounds):
-    for d in (0, 1):
+    for d in DIRS:
         for i, shp in enumerate(shapes):
             apply(d, shp)
             for j in range(reps + 1):
