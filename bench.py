@@ -18,6 +18,12 @@ stream the kernels run on, inside the timed region. Algorithmic bytes: 20 B/elem
 (encode: 4 read + 16 written; decode: 16 read + 4 written), SURVEY.md §8(d).
 cpu_baseline: the reference CPU op restated (oracle/: encode loop + GMP mpf decode, TF-Shard-like
 contiguous blocks over host threads) timed on this box on the same tensor (rank 0, N = 1 only).
+
+    python bench.py --stage p      Stage P report (SURVEY.md §8(d) last row), one JSON line per key:
+Paillier encrypt (fresh randomness through the fixed-base table) and CRT decrypt of int64
+mantissas on one GPU, elements/s, against the VALU roofline (32x32->64 multiply-accumulates of the
+Montgomery products vs the measured v_mad_u64_u32 issue rate), beside the reference's GMP path
+(oracle/paillier_gmp.c pl_gmp_bench: key state built once, threads like TF Shard) on this box.
 """
 from __future__ import annotations
 
@@ -51,6 +57,8 @@ def parse():
     p.add_argument("--tune", default=os.environ.get("EFL_FXP_TUNE", ""),
                    help="comma list kind=value for efl_fxp_tune (variant exploration)")
     p.add_argument("--rows", type=int, default=ROWS)
+    p.add_argument("--stage", choices=("f", "p"), default="f",
+                   help="f: the BASELINE.json metric (fixed-point codec); p: the Paillier report")
     return p.parse_args()
 
 
@@ -106,8 +114,121 @@ def cpu_baseline(x_dev, threads):
             "ms_per_step": round(t * 1e3, 2)}
 
 
+# ------------------------------------------------------------------------------------ Stage P
+# v_mad_u64_u32 issue rate measured on MI355X (tools/valu_probe.hip -> profiles/r01/valu_probe.jsonl:
+# 2.77e13 lane-ops/s with every CU busy). Every 32x32 limb product of a Montgomery multiplication
+# is one such instruction, so MAC/s / this rate is the kernel's VALU roofline fraction.
+MAD_U64_U32_PEAK = 2.7691e13
+# (label, n_bytes, a_bytes, group_size, elements): the paillier_mnist example key
+# (efls-train/python/efl/example/paillier_mnist/follower_dense.py:39, a_bytes = n_bytes/2 as
+# paillier.py:175-176) and the reference default key (paillier.cc:799-805 / paillier.py:173-176)
+STAGE_P_KEYS = [("example 1024-bit n, group_size 10", 128, 64, 10, 262144),
+                ("example 1024-bit n, group_size 10, MNIST activation [256, 392]", 128, 64, 10, 256 * 392),
+                ("default 4096-bit n, group_size 1", 512, 256, 1, 65536)]
+
+
+def _mont_macs(L, squarings, multiplies):
+    """32x32 MACs of CIOS Montgomery products over L limbs: 2 L^2 per product."""
+    return 2 * L * L * (squarings + multiplies)
+
+
+def stage_p(args):
+    import random
+    import efl
+    from efl.privacy import paillier_cipher as pc
+    dev = efl.lib.require_gpu()
+    lib = efl.lib.raw()
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+    cpu_keys = {}
+    for label, n_bytes, a_bytes, g, N in STAGE_P_KEYS:
+        n, hs, p, q = pc.generate_keypair_ints(n_bytes, 24, random.Random(n_bytes))
+        kp = efl.paillier.Keypair(seed=7)
+        kp.set_keys_ints(n, hs, a_bytes, g, p, q, n_bytes)
+        k = kp.key
+        gen = torch.Generator(device=dev).manual_seed(0)
+        m = torch.randint(-2**40, 2**40, (N,), dtype=torch.int64, device=dev, generator=gen)
+        ct = torch.empty((N, k.lc), dtype=torch.int32, device=dev)
+        mag = torch.empty((N, k.ln), dtype=torch.int32, device=dev)
+        neg = torch.empty(N, dtype=torch.int8, device=dev)
+
+        def enc():
+            efl.lib.check(lib.efl_pl_encrypt(*k.args(), m.data_ptr(), None, ct.data_ptr(), N, 7, 0, sh))
+
+        def dec():
+            efl.lib.check(lib.efl_pl_decrypt(*k.args(), ct.data_ptr(), mag.data_ptr(), neg.data_ptr(), N, sh))
+
+        times = {}
+        for name, fn in (("encrypt", enc), ("decrypt", dec)):
+            for _ in range(max(1, args.warmup // 5)):
+                fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            reps = 3
+            e0.record(stream)
+            for _ in range(reps):
+                fn()
+            e1.record(stream)
+            e1.synchronize()
+            times[name] = e0.elapsed_time(e1) / reps * 1e-3
+        got = kp.decrypt(pc.CipherTensor(ct[:512], (512,), k), dtype=torch.int64)
+        if not torch.equal(got, m[:512]):
+            raise SystemExit("bench: Paillier round trip is wrong")
+        # work per element (exact for decrypt's uniform exponents; expected value for the table)
+        pm1, qm1 = p - 1, q - 1
+        dec_macs = sum(_mont_macs(k.ln, e.bit_length() - 1, bin(e).count("1") - 1) for e in (pm1, qm1))
+        rows = -(-8 * a_bytes // g)
+        enc_macs = _mont_macs(k.lc, 0, rows * (1 - 2.0 ** -g) + 1)
+        res = {}
+        for name, macs in (("encrypt", enc_macs), ("decrypt", dec_macs)):
+            per_s = N / times[name]
+            res[name] = {"elements_per_s": round(per_s), "ms": round(times[name] * 1e3, 3),
+                         "macs_per_element": int(macs),
+                         "roofline": {"bound": "valu", "achieved": round(per_s * macs / 1e12, 3),
+                                      "peak": round(MAD_U64_U32_PEAK / 1e12, 3), "unit": "TMAC/s",
+                                      "frac": round(per_s * macs / MAD_U64_U32_PEAK, 4)},
+                         "kernel_family": pc.kernel_slicing(k.ln, name == "decrypt")}
+        out = {"metric": "Paillier elements/s on 1 GPU (encrypt with fresh randomness, CRT decrypt)",
+               "stage": "P", "config": {"key": label, "n_bits": 8 * n_bytes, "a_bits": 8 * a_bytes,
+                                        "group_size": g, "elements": N},
+               "unit": "elements/s", "higher_is_better": True, "dtype": "u32 limbs",
+               "data": "synthetic int64 mantissas in [-2^40, 2^40), deterministic key", **res,
+               "cpu_baseline": None}
+        if not args.no_cpu_baseline:
+            out["cpu_baseline"] = stage_p_cpu(n_bytes, a_bytes, g, p, q, hs, args.cpu_threads, cpu_keys)
+            for name in ("encrypt", "decrypt"):
+                out[name]["vs_cpu"] = round(out[name]["elements_per_s"] / out["cpu_baseline"][name], 1)
+        print(json.dumps(out), flush=True)
+
+
+def stage_p_cpu(n_bytes, a_bytes, g, p, q, hs, threads, cache):
+    """The reference's GMP path (oracle/paillier_gmp.c pl_gmp_bench) on a bounded sample sized for
+    a few seconds per op on `threads` host threads."""
+    import ctypes
+    from oracle import fxp, paillier as P
+    L = fxp.lib()
+    L.pl_gmp_bench.argtypes = [ctypes.c_char_p] * 3 + [ctypes.c_uint, ctypes.c_uint, ctypes.c_longlong,
+                                                        ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+    key = (n_bytes, a_bytes, g)
+    if key in cache:
+        return cache[key]
+    t = (ctypes.c_double * 2)()
+    count = threads * 4
+    while True:
+        L.pl_gmp_bench(P.hx(p).encode(), P.hx(q).encode(), P.hx(hs).encode(), 8 * a_bytes, g, count, threads, t)
+        if t[1] > 2.0 or count >= 1 << 20:
+            break
+        count = min(1 << 20, int(count * min(16.0, max(2.0, 4.0 / max(t[1], 1e-3)))))
+    cache[key] = {"encrypt": round(count / t[0], 1), "decrypt": round(count / t[1], 1), "unit": "elements/s",
+                  "cores": threads, "kind": "port",
+                  "sample": f"{count} elements, GMP mpz path of paillier.cc:103-131 / :296-312 with the "
+                            f"fbpowm table of gmp_utils.cc:56-144 built once, {threads} threads"}
+    return cache[key]
+
+
 def main():
     args = parse()
+    if args.stage == "p":
+        return stage_p(args)
     world, rank, local = setup_dist(args)
     import efl
     dev = efl.lib.require_gpu()

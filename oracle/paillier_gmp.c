@@ -210,3 +210,165 @@ EFL_EXPORT void pl_gmp_powm(const char* b_hex, const char* e_hex, const char* m_
   put(out, cap, r);
   mpz_clears(b, e, m, r, NULL);
 }
+
+/* ------------------------------------------------------------------------------------------
+ * CPU baseline of Stage P (bench.py --stage p, cpu_baseline leg only): the reference's per-element
+ * work with the key state built ONCE, as the PaillierKeypair resource holds it (paillier.cc:70-101:
+ * n^2, hp, hq, q^-1 mod p, the fbpowm table of gmp_utils.cc:56-89), then `count` encryptions with
+ * fresh randomness (urandomb a of a_bits, fbpowm, (1+|m|n)^(+-1) * hsa mod n^2; paillier.cc:103-131)
+ * and `count` CRT decryptions (paillier.cc:296-312), split into contiguous blocks over `threads`
+ * pthreads like TF Shard. Each thread owns its MT state (the reference shares one, unlocked).
+ * times[0] = encrypt seconds, times[1] = decrypt seconds (wall).
+ * ------------------------------------------------------------------------------------------ */
+#include <pthread.h>
+#include <time.h>
+
+typedef struct {
+  mpz_t n, n2, p, q, p2, q2, hp, hq, qinv, mx;
+  mpz_t* T;
+  unsigned long long cols;
+  unsigned rows, g, a_bits;
+} bench_key;
+
+typedef struct {
+  bench_key* k;
+  long long lo, hi;
+  int op;   /* 0 encrypt, 1 decrypt */
+  char** cts;
+  unsigned long seed;
+} bench_job;
+
+static void bench_fbpowm(mpz_t acc, const bench_key* k, const mpz_t a) {
+  const size_t size = mpz_sgn(a) ? mpz_sizeinbase(a, 2) : 1;
+  mpz_set_ui(acc, 1);
+  for (size_t s = 0, row = 0; s < size; s += k->g, ++row) {
+    const size_t w = size - s < k->g ? size - s : k->g;
+    unsigned long idx = 0;
+    for (size_t j = 0; j < w; ++j) idx = (idx << 1) | (unsigned long)mpz_tstbit(a, s + j);
+    if (idx) {
+      mpz_mul(acc, acc, k->T[row * k->cols + idx - 1]);
+      mpz_mod(acc, acc, k->n2);
+    }
+  }
+}
+
+static void* bench_worker(void* arg) {
+  bench_job* jb = (bench_job*)arg;
+  bench_key* k = jb->k;
+  mpz_t a, h, c, m, cq;
+  mpz_inits(a, h, c, m, cq, NULL);
+  gmp_randstate_t st;
+  gmp_randinit_mt(st);
+  gmp_randseed_ui(st, jb->seed);
+  for (long long i = jb->lo; i < jb->hi; ++i) {
+    if (jb->op == 0) {
+      long long mv = (i * 2654435761LL) % 1000003LL - 500001LL;
+      mpz_urandomb(a, st, k->a_bits);
+      bench_fbpowm(h, k, a);
+      unsigned long long u = mv < 0 ? 0ull - (unsigned long long)mv : (unsigned long long)mv;
+      mpz_import(c, 1, -1, sizeof(u), 0, 0, &u);
+      mpz_mul(c, c, k->n);
+      mpz_add_ui(c, c, 1);
+      if (mv < 0) mpz_invert(c, c, k->n2);
+      mpz_mul(c, c, h);
+      mpz_mod(c, c, k->n2);
+      char* s = mpz_get_str(NULL, 16, c);   /* the op's DT_STRING output */
+      if (jb->cts) jb->cts[i] = s;
+      else {
+        void (*freefunc)(void*, size_t);
+        mp_get_memory_functions(NULL, NULL, &freefunc);
+        freefunc(s, strlen(s) + 1);
+      }
+    } else {
+      mpz_set_str(c, jb->cts[i], 16);
+      m_func(m, c, k->p, k->p2, k->hp);
+      m_func(cq, c, k->q, k->q2, k->hq);
+      mpz_sub(m, m, cq);
+      mpz_mul(m, m, k->qinv);
+      mpz_mod(m, m, k->p);
+      mpz_mul(m, m, k->q);
+      mpz_add(m, m, cq);
+      mpz_mod(m, m, k->n);
+      if (mpz_cmp(m, k->mx) > 0) mpz_sub(m, m, k->n);
+      char* s = mpz_get_str(NULL, 16, m);
+      void (*freefunc)(void*, size_t);
+      mp_get_memory_functions(NULL, NULL, &freefunc);
+      freefunc(s, strlen(s) + 1);
+    }
+  }
+  gmp_randclear(st);
+  mpz_clears(a, h, c, m, cq, NULL);
+  return NULL;
+}
+
+static double now_s(void) {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
+static void bench_run(bench_key* k, int op, char** cts, long long count, int threads) {
+  pthread_t th[256];
+  bench_job jobs[256];
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  for (int t = 0; t < threads; ++t) {
+    jobs[t].k = k;
+    jobs[t].op = op;
+    jobs[t].cts = cts;
+    jobs[t].lo = count * t / threads;
+    jobs[t].hi = count * (t + 1) / threads;
+    jobs[t].seed = 12345ul + (unsigned long)t;
+    pthread_create(&th[t], NULL, bench_worker, &jobs[t]);
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+}
+
+EFL_EXPORT void pl_gmp_bench(const char* p_hex, const char* q_hex, const char* hs_hex, unsigned a_bits,
+                             unsigned g, long long count, int threads, double* times) {
+  bench_key k;
+  mpz_inits(k.n, k.n2, k.p, k.q, k.p2, k.q2, k.hp, k.hq, k.qinv, k.mx, NULL);
+  mpz_set_str(k.p, p_hex, 16);
+  mpz_set_str(k.q, q_hex, 16);
+  mpz_mul(k.n, k.p, k.q);
+  mpz_mul(k.n2, k.n, k.n);
+  mpz_mul(k.p2, k.p, k.p);
+  mpz_mul(k.q2, k.q, k.q);
+  h_func(k.hp, k.n, k.p, k.p2);
+  h_func(k.hq, k.n, k.q, k.q2);
+  mpz_invert(k.qinv, k.q, k.p);
+  mpz_mul_2exp(k.mx, k.n, 1);
+  mpz_cdiv_q_ui(k.mx, k.mx, 3);
+  k.g = g;
+  k.a_bits = a_bits;
+  k.cols = (1ull << g) - 1;
+  k.rows = a_bits / g + (a_bits % g ? 1 : 0);
+  k.T = (mpz_t*)malloc(sizeof(mpz_t) * k.rows * k.cols);
+  mpz_t hs;
+  mpz_init_set_str(hs, hs_hex, 16);
+  for (unsigned long long i = 0; i < k.rows * k.cols; ++i) mpz_init(k.T[i]);
+  mpz_set(k.T[0], hs);
+  for (unsigned long long j = 1; j < k.cols; ++j) {
+    mpz_mul(k.T[j], k.T[j - 1], hs);
+    mpz_mod(k.T[j], k.T[j], k.n2);
+  }
+  for (unsigned i = 1; i < k.rows; ++i)
+    for (unsigned long long j = 0; j < k.cols; ++j)
+      mpz_powm_ui(k.T[i * k.cols + j], k.T[(i - 1) * k.cols + j], 1ul << g, k.n2);
+  char** cts = (char**)calloc((size_t)count, sizeof(char*));
+  double t0 = now_s();
+  bench_run(&k, 0, cts, count, threads);
+  times[0] = now_s() - t0;
+  t0 = now_s();
+  bench_run(&k, 1, cts, count, threads);
+  times[1] = now_s() - t0;
+  void (*freefunc)(void*, size_t);
+  mp_get_memory_functions(NULL, NULL, &freefunc);
+  for (long long i = 0; i < count; ++i)
+    if (cts[i]) freefunc(cts[i], strlen(cts[i]) + 1);
+  free(cts);
+  for (unsigned long long i = 0; i < k.rows * k.cols; ++i) mpz_clear(k.T[i]);
+  free(k.T);
+  mpz_clear(hs);
+  mpz_clears(k.n, k.n2, k.p, k.q, k.p2, k.q2, k.hp, k.hq, k.qinv, k.mx, NULL);
+}
