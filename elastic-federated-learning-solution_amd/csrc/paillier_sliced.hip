@@ -12,6 +12,7 @@
 // same word (broadcast); the E elements of the wave hit consecutive banks.
 #include "pl_common.h"
 #include "sliced.h"
+#include "sliced28.h"
 
 namespace efl {
 namespace pl {
@@ -129,6 +130,12 @@ __device__ __forceinline__ void fbpowm_mont(uint32_t (&acc)[C], const Key& k, co
 #define SL_OCC __attribute__((amdgpu_waves_per_eu(C == 16 ? EFL_SL_WAVES16 : EFL_SL_WAVES32)))
 #else
 #define SL_OCC
+#endif
+
+// Minimum waves per SIMD for the decryption kernels (caps their VGPRs at 512 / EFL_DEC_WAVES):
+// the radix-2^28 exponentiation needs latency hiding across waves more than registers.
+#ifndef EFL_DEC_WAVES
+#define EFL_DEC_WAVES 4
 #endif
 
 #define SL_ELEMENT(E_, G_)                                   \
@@ -335,13 +342,37 @@ __device__ __forceinline__ void m_func(uint32_t (&res)[C / 2], const uint32_t* _
   redc<C, G>(lo, x2, x2_minv, g);                   // lo R
   const uint32_t top = add<C, G>(t, lo, g);
   csub<C, G>(t, x2, top != 0 || geq<C, G>(t, x2, g), g);
-  to_lds<C>(BASE, E, g, t);
+  // The exponentiation runs in radix 2^28 with lazy carries (csrc/sliced28.h: one v_mad_u64_u32
+  // per limb product instead of about three instructions): c mod x^2 in normal form -> 28-bit
+  // limbs through LDS -> c R28 mod x^2 -> square-and-multiply by x - 1 -> redc (< x^2) -> 32-bit.
+  constexpr int C28 = s28::limbs_per_lane(L, G), L28 = C28 * G;
+  constexpr int kLog2G = G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3 : G == 16 ? 4 : 5;
+  redc<C, G>(t, x2, x2_minv, g);   // c mod x^2
+  to_lds<C>(SCR, E, g, t);
+  lds_sync();
+  // keep the key constants the code after the exponentiation needs from being loaded (and held
+  // in VGPRs) across it: the loop wants its registers for the accumulators
+  asm volatile("" ::: "memory");
+  uint32_t a[C28], m28[C28];
+  s28::from_words<C28>(a, SCR, E, L, g);
+  slice_uniform<C28>(m28, k.at(second ? k.d.off_q2_28 : k.d.off_p2_28), g);
+  const uint32_t minv28 = second ? k.d.q2_minv28 : k.d.p2_minv28;
+  s28::mont_mul<C28, G>(a, Uniform{k.at(second ? k.d.off_q2_r2_28[kLog2G] : k.d.off_p2_r2_28[kLog2G])}, m28,
+                        minv28, g);
+  lds_sync();
+  to_lds<C28>(BASE, E, g, a);
 #pragma unroll 1
   for (int b = ebits - 2; b >= 0; --b) {
-    mont_sqr<C, G>(t, SCR, E, x2, x2_minv, g);
-    if ((ex[b >> 5] >> (b & 31)) & 1u) mont_mul<C, G>(t, LdsElem{BASE, E}, x2, x2_minv, g);
+    s28::mont_sqr<C28, G>(a, SCR, E, m28, minv28, g);
+    if ((ex[b >> 5] >> (b & 31)) & 1u) s28::mont_mul<C28, G>(a, LdsElem{BASE, E}, m28, minv28, g);
   }
-  redc<C, G>(t, x2, x2_minv, g);   // y = c^(x-1) mod x^2  (y = 1 mod x, so y >= 1)
+  s28::mont_mul<C28, G>(a, Unit{}, m28, minv28, g);   // y = c^(x-1) mod x^2 (< x^2; y = 1 mod x, so y >= 1)
+  lds_sync();
+  to_lds<C28>(SCR, E, g, a);
+  lds_sync();
+  s28::to_words<C>(t, SCR, E, L28, g);
+  lds_sync();
+  asm volatile("" ::: "memory");
   sub_small<C, G>(t, 1u, g);
   to_lds<C>(SCR, E, g, t);
   lds_sync();
@@ -382,15 +413,16 @@ __device__ __forceinline__ void m_func(uint32_t (&res)[C / 2], const uint32_t* _
 }
 
 template <int C, int G>
-__global__ __launch_bounds__(kSlBlock) SL_OCC void k_decrypt(Key k, const uint32_t* __restrict__ ct,
+__global__ __launch_bounds__(kSlBlock, EFL_DEC_WAVES) void k_decrypt(Key k, const uint32_t* __restrict__ ct,
                                                       uint32_t* __restrict__ mag, signed char* __restrict__ neg,
                                                       long long N) {
   constexpr int L = C * G, E = kSlBlock / G, CH = C / 2, LH = L / 2;
+  constexpr int L28 = s28::limbs_per_lane(L, G) * G;   // LDS arrays also hold radix-2^28 numbers
   extern __shared__ uint32_t lds[];
   SL_ELEMENT(E, G)
   if (i >= N) return;
   uint32_t* BASE = lds + e;
-  uint32_t* SCR = lds + L * E + e;
+  uint32_t* SCR = lds + L28 * E + e;
   const uint32_t* c = ct + i * 2 * L;
   uint32_t mp[CH], mq[CH];
   m_func<C, G>(mp, c, k, false, BASE, SCR, E, g);
@@ -500,7 +532,8 @@ hipError_t run_matmul(const Key& k, const uint32_t* X, const long long* xe, cons
 template <int C, int G>
 hipError_t run_decrypt(const Key& k, const uint32_t* ct, uint32_t* mag, signed char* neg, long long N,
                        hipStream_t s) {
-  hipLaunchKernelGGL((k_decrypt<C, G>), dim3(grid_of(N, G)), dim3(kSlBlock), (size_t)(2 * C * G) * (kSlBlock / G) * 4, s, k, ct,
+  hipLaunchKernelGGL((k_decrypt<C, G>), dim3(grid_of(N, G)), dim3(kSlBlock),
+                     (size_t)(2 * s28::limbs_per_lane(C * G, G) * G) * (kSlBlock / G) * 4, s, k, ct,
                      mag, neg, N);
   return hipGetLastError();
 }

@@ -22,12 +22,46 @@ namespace sl {
 
 __device__ __forceinline__ uint64_t mad(uint32_t a, uint32_t b, uint64_t c) { return (uint64_t)a * b + c; }
 
+// Cross-lane moves inside aligned groups of G lanes. The two on every CIOS step (bcast0,
+// from_next) are DPP moves (one VALU instruction, no LDS round trip) wherever one instruction
+// does it; ds_bpermute (__shfl) otherwise. DPP controls (GFX9 encoding): quad_perm 0x00-0xFF,
+// row_shl:1 0x101 (lane i <- i+1 in its 16-lane row), row_shr:1 0x111, row_shr:4 0x114,
+// wave_shl:1 0x130, wave_shr:1 0x138, row_newbcast:0 0x150 (lane 0 of the row to the row).
 template <int G>
-__device__ __forceinline__ uint32_t bcast0(uint32_t v) { return G == 1 ? v : __shfl(v, 0, G); }
+__device__ __forceinline__ uint32_t bcast0(uint32_t v) {
+  if constexpr (G == 1) {
+    return v;
+  } else if constexpr (G == 2) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xA0, 0xF, 0xF, false);   // quad_perm [0,0,2,2]
+  } else if constexpr (G == 4) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x00, 0xF, 0xF, false);   // quad_perm [0,0,0,0]
+  } else if constexpr (G == 8) {
+    // lane 0 of every quad, then the upper quad of each 8-lane group (banks 1, 3) copies the
+    // lower quad's value from 4 lanes down
+    const int q = __builtin_amdgcn_mov_dpp((int)v, 0x00, 0xF, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_update_dpp(q, q, 0x114, 0xF, 0xA, false);
+  } else if constexpr (G == 16) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x150, 0xF, 0xF, false);  // row_newbcast:0
+  } else {
+    return __shfl(v, 0, G);
+  }
+}
+// lane g <- lane g+1 (the caller zeroes lane G-1)
 template <int G>
-__device__ __forceinline__ uint32_t from_next(uint32_t v) { return G == 1 ? 0u : __shfl_down(v, 1, G); }
+__device__ __forceinline__ uint32_t from_next(uint32_t v) {
+  if constexpr (G == 1) return 0u;
+  else if constexpr (G <= 16) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x101, 0xF, 0xF, true);
+  else if constexpr (G == 32) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xF, 0xF, true);
+  else return __shfl_down(v, 1, G);
+}
+// lane g <- lane g-1 (the caller zeroes lane 0)
 template <int G>
-__device__ __forceinline__ uint32_t from_prev(uint32_t v) { return G == 1 ? 0u : __shfl_up(v, 1, G); }
+__device__ __forceinline__ uint32_t from_prev(uint32_t v) {
+  if constexpr (G == 1) return 0u;
+  else if constexpr (G <= 16) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x111, 0xF, 0xF, true);
+  else if constexpr (G == 32) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xF, 0xF, true);
+  else return __shfl_up(v, 1, G);
+}
 template <int G>
 __device__ __forceinline__ uint32_t from_lane(uint32_t v, int src) { return G == 1 ? v : __shfl(v, src, G); }
 

@@ -38,7 +38,10 @@ class PlKey(ctypes.Structure):
                [(n, ctypes.c_int64) for n in ("off_n", "off_n2", "off_n2_r2", "off_n2_one", "off_table", "off_max",
                                                "off_p", "off_q", "off_p2", "off_q2", "off_p2_r3", "off_q2_r3",
                                                "off_pm1", "off_qm1", "off_pinv_w", "off_qinv_w", "off_hp",
-                                               "off_hq", "off_qinvp")]
+                                               "off_hq", "off_qinvp")] + \
+               [("p2_28_len", ctypes.c_int32), ("p2_minv28", ctypes.c_uint32), ("q2_minv28", ctypes.c_uint32),
+                ("off_p2_28", ctypes.c_int64), ("off_q2_28", ctypes.c_int64),
+                ("off_p2_r2_28", ctypes.c_int64 * 6), ("off_q2_r2_28", ctypes.c_int64 * 6)]
 
 
 _PK = ctypes.POINTER(PlKey)
@@ -91,6 +94,17 @@ def _limbs(x: int, L: int) -> np.ndarray:
 
 def _minv32(m: int) -> int:
     return (-pow(m, -1, 1 << 32)) % (1 << 32)
+
+
+def _limbs28(x: int, L: int) -> np.ndarray:
+    """x as L radix-2^28 limbs, one per 32-bit word (csrc/sliced28.h)."""
+    return np.array([(x >> (28 * k)) & 0xFFFFFFF for k in range(L)], dtype="<u4")
+
+
+def limbs28_total(ln: int, G: int) -> int:
+    """Limbs of the radix-2^28 form the sliced kernels use for an ln-word modulus over G lanes
+    (s28::limbs_per_lane(ln, G) * G: R = 2^(28 L) > 4 m)."""
+    return ((32 * ln + 2 + 27) // 28 + G - 1) // G * G
 
 
 def _hex_of(v) -> str:
@@ -231,6 +245,22 @@ class KeyBlock:
             d.off_hp = put(hp * Rh % p, self.lh)
             d.off_hq = put(hq * Rh % q, self.lh)
             d.off_qinvp = put(pow(q, -1, p) * Rh % p, self.lh)
+            # radix-2^28 constants for the sliced decryption (include/efl_hip.h, csrc/sliced28.h)
+            L28s = [limbs28_total(ln, 1 << k) for k in range(6)]
+            Lmax = max(L28s)
+            d.p2_28_len = Lmax
+
+            def put28(x: int) -> int:
+                off = pos[0]
+                words.append(_limbs28(x, Lmax))
+                pos[0] += Lmax
+                return off
+            d.off_p2_28, d.off_q2_28 = put28(p * p), put28(q * q)
+            d.p2_minv28 = (-pow(p * p, -1, 1 << 28)) % (1 << 28)
+            d.q2_minv28 = (-pow(q * q, -1, 1 << 28)) % (1 << 28)
+            for k, L28 in enumerate(L28s):
+                d.off_p2_r2_28[k] = put28(pow(2, 2 * 28 * L28, p * p))
+                d.off_q2_r2_28[k] = put28(pow(2, 2 * 28 * L28, q * q))
         # fixed-base table T[i][j] = hs^((j+1) 2^(g i)) mod n^2, Montgomery form (gmp_utils.cc:56-89)
         g = group_size
         cols = (1 << g) - 1

@@ -154,6 +154,16 @@ typedef struct {
   int64_t off_n, off_n2, off_n2_r2, off_n2_one, off_table, off_max;
   int64_t off_p, off_q, off_p2, off_q2, off_p2_r3, off_q2_r3, off_pm1, off_qm1;
   int64_t off_pinv_w, off_qinv_w, off_hp, off_hq, off_qinvp;
+  /* Radix-2^28 constants of the decryption exponentiations (sliced kernels, csrc/sliced28.h):
+   *   off_p2_28    p^2 as 28-bit limbs (one per 32-bit word), zero-padded to p2_28_len limbs
+   *   p2_minv28    -p^2^-1 mod 2^28 (likewise q)
+   *   off_p2_r2_28[k]  R28^2 mod p^2 as p2_28_len 28-bit limbs, R28 = 2^(28 L28) for the kernels
+   *                that spread a number over G = 2^k lanes, L28 = G * ceil(ceil((32 ln + 2) / 28) / G)
+   * has_private == 0 leaves them unused. */
+  int32_t p2_28_len;
+  uint32_t p2_minv28, q2_minv28;
+  int64_t off_p2_28, off_q2_28;
+  int64_t off_p2_r2_28[6], off_q2_r2_28[6];
 } efl_pl_key;
 
 /*
