@@ -115,10 +115,13 @@ def cpu_baseline(x_dev, threads):
 
 
 # ------------------------------------------------------------------------------------ Stage P
-# v_mad_u64_u32 issue rate measured on MI355X (tools/valu_probe.hip -> profiles/r01/valu_probe.jsonl:
-# 2.77e13 lane-ops/s with every CU busy). Every 32x32 limb product of a Montgomery multiplication
-# is one such instruction, so MAC/s / this rate is the kernel's VALU roofline fraction.
-MAD_U64_U32_PEAK = 2.7691e13
+# v_mad_u64_u32 issue rate measured on MI355X with every CU busy, in the shape of a Montgomery row
+# (24 64-bit accumulators, one uniform multiplier): 3.17e13 lane-ops/s (tools/valu_probe.hip ->
+# profiles/r01/valu_probe.jsonl). Every limb product of a Montgomery multiplication is one such
+# instruction. `achieved` counts the algorithm's 32x32-bit limb products (radix-independent work),
+# `limb_products_per_s` the instructions the kernel really issues (radix-2^28 decryption issues
+# (32/28)^2 more, smaller ones).
+MAD_U64_U32_PEAK = 3.1722e13
 # (label, n_bytes, a_bytes, group_size, elements): the paillier_mnist example key
 # (efls-train/python/efl/example/paillier_mnist/follower_dense.py:39, a_bytes = n_bytes/2 as
 # paillier.py:175-176) and the reference default key (paillier.cc:799-805 / paillier.py:173-176)
@@ -181,12 +184,19 @@ def stage_p(args):
         res = {}
         for name, macs in (("encrypt", enc_macs), ("decrypt", dec_macs)):
             per_s = N / times[name]
+            fam = pc.kernel_slicing(k.ln, name == "decrypt")
+            issued = macs
+            if name == "decrypt" and fam:     # sliced decryption exponentiates in radix 2^28
+                L28 = pc.limbs28_total(k.ln, k.ln // fam)
+                issued = sum(_mont_macs(L28, e.bit_length() - 1, bin(e).count("1") - 1) for e in (pm1, qm1))
             res[name] = {"elements_per_s": round(per_s), "ms": round(times[name] * 1e3, 3),
                          "macs_per_element": int(macs),
                          "roofline": {"bound": "valu", "achieved": round(per_s * macs / 1e12, 3),
                                       "peak": round(MAD_U64_U32_PEAK / 1e12, 3), "unit": "TMAC/s",
-                                      "frac": round(per_s * macs / MAD_U64_U32_PEAK, 4)},
-                         "kernel_family": pc.kernel_slicing(k.ln, name == "decrypt")}
+                                      "frac": round(per_s * macs / MAD_U64_U32_PEAK, 4),
+                                      "limb_products_per_s": round(per_s * issued / 1e12, 3),
+                                      "issue_frac": round(per_s * issued / MAD_U64_U32_PEAK, 4)},
+                         "kernel_family": fam}
         out = {"metric": "Paillier elements/s on 1 GPU (encrypt with fresh randomness, CRT decrypt)",
                "stage": "P", "config": {"key": label, "n_bits": 8 * n_bytes, "a_bits": 8 * a_bytes,
                                         "group_size": g, "elements": N},

@@ -726,7 +726,7 @@ inline bool key_ok(const efl_pl_key* d, bool need_private, int ln_max) {
 
 // kernel family per key size: 0 = one lane per element (paillier.hip), C = sliced over 2ln/C (n^2
 // ops) or ln/C (decryption) lanes of C limbs (paillier_sliced.hip). [ln 16/32/64/128][n^2 ops, decrypt]
-int g_slicing[4][2] = {{16, 8}, {16, 16}, {16, 8}, {8, 8}};   // measured: profiles/r01/bench_pl*.jsonl
+int g_slicing[4][2] = {{16, 8}, {16, 32}, {16, 32}, {8, 32}};   // measured: profiles/r01/bench_pl*.jsonl
 inline int ln_index(int ln) { return ln == 16 ? 0 : ln == 32 ? 1 : ln == 64 ? 2 : 3; }
 inline int slicing(int ln, int dec) { return g_slicing[ln_index(ln)][dec]; }
 

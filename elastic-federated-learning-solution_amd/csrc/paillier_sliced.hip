@@ -132,7 +132,8 @@ __device__ __forceinline__ void fbpowm_mont(uint32_t (&acc)[C], const Key& k, co
 #define SL_OCC
 #endif
 
-// Minimum waves per SIMD for the decryption kernels (caps their VGPRs at 512 / EFL_DEC_WAVES):
+// Minimum waves per SIMD for the decryption kernels with C <= 16 limbs per lane (caps their VGPRs
+// at 512 / EFL_DEC_WAVES; C = 32 keeps 2 waves, it spills heavily below 256 VGPRs):
 // the radix-2^28 exponentiation needs latency hiding across waves more than registers.
 #ifndef EFL_DEC_WAVES
 #define EFL_DEC_WAVES 4
@@ -413,7 +414,7 @@ __device__ __forceinline__ void m_func(uint32_t (&res)[C / 2], const uint32_t* _
 }
 
 template <int C, int G>
-__global__ __launch_bounds__(kSlBlock, EFL_DEC_WAVES) void k_decrypt(Key k, const uint32_t* __restrict__ ct,
+__global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_decrypt(Key k, const uint32_t* __restrict__ ct,
                                                       uint32_t* __restrict__ mag, signed char* __restrict__ neg,
                                                       long long N) {
   constexpr int L = C * G, E = kSlBlock / G, CH = C / 2, LH = L / 2;
@@ -544,7 +545,7 @@ hipError_t run_decrypt(const Key& k, const uint32_t* ct, uint32_t* mag, signed c
 bool sliced_available(int L, int C) {
   switch (L * 1000 + C) {
     case 16008: case 32008: case 64008: case 128008: case 256008:
-    case 32016: case 64016: case 64032: case 128016: case 128032: case 256016: case 256032: return true;
+    case 32016: case 32032: case 64016: case 64032: case 128016: case 128032: case 256016: case 256032: return true;
     default: return false;
   }
 }
@@ -557,6 +558,7 @@ bool sliced_available(int L, int C) {
     case 128008: { constexpr int CC = 8, GG = 16; return EXPR; } \
     case 256008: { constexpr int CC = 8, GG = 32; return EXPR; } \
     case 32016: { constexpr int CC = 16, GG = 2; return EXPR; }  \
+    case 32032: { constexpr int CC = 32, GG = 1; return EXPR; }  \
     case 64016: { constexpr int CC = 16, GG = 4; return EXPR; }  \
     case 64032: { constexpr int CC = 32, GG = 2; return EXPR; }  \
     case 128016: { constexpr int CC = 16, GG = 8; return EXPR; } \

@@ -81,7 +81,7 @@ def set_kernel_slicing(ln: int, decrypt: bool, limbs_per_lane: int) -> int:
 
 
 # kernel families compiled per key size (ln): n^2 ops, decryption
-SLICINGS = {16: ([0, 8, 16], [0, 8]), 32: ([0, 8, 16, 32], [0, 8, 16]), 64: ([0, 8, 16, 32], [0, 8, 16, 32]),
+SLICINGS = {16: ([0, 8, 16, 32], [0, 8]), 32: ([0, 8, 16, 32], [0, 8, 16, 32]), 64: ([0, 8, 16, 32], [0, 8, 16, 32]),
             128: ([8, 16, 32], [0, 8, 16, 32])}
 
 _LIMB_CLASSES = (16, 32, 64, 128)

@@ -3,9 +3,11 @@
 // the Paillier kernels are VALU-bound, and the relevant peak is the rate of the 32x32->64
 // multiply-accumulate (v_mad_u64_u32), not an HBM or MFMA number.
 //
-// Each kernel runs 8 independent dependency chains per lane (enough ILP to saturate issue) for
-// `iters` iterations; grid = 8 workgroups of 256 lanes per CU. Reported per op: lane-ops/s and
-// lane-ops per clock per CU at the measured shader clock (s_memtime ticks / wall).
+// Each kernel runs kChains independent dependency chains per lane for `iters` iterations; grid = 8
+// workgroups of 256 lanes per CU. v_mad_u64_u32 is also run with 24 chains and a wave-uniform
+// multiplier (the shape of a Montgomery row: one b limb times many a limbs into 64-bit
+// accumulators), which is what saturates its issue. Reported per op: lane-ops/s and lane-ops per
+// clock per CU at 2.4 GHz.
 //
 //   hipcc -O3 --offload-arch=gfx950 -o tools/valu_probe tools/valu_probe.hip && tools/valu_probe
 #include <hip/hip_runtime.h>
@@ -25,9 +27,12 @@
 
 constexpr int kChains = 8;
 
-enum Op { MAD_U64_U32 = 0, MUL_LO_U32, MUL_HI_U32, ADD_CO_PAIR, FMA_F64, MAD_U32_U24, FMA_F32, LSHL_ADD_U64, kOps };
+enum Op { MAD_U64_U32 = 0, MUL_LO_U32, MUL_HI_U32, ADD_CO_PAIR, FMA_F64, MAD_U32_U24, FMA_F32, LSHL_ADD_U64,
+          MAD_ROW, kOps };
 const char* kNames[kOps] = {"v_mad_u64_u32", "v_mul_lo_u32", "v_mul_hi_u32", "add_co_u32+addc_co_u32",
-                            "v_fma_f64", "v_mad_u32_u24", "v_fma_f32", "u64 add (v_lshl_add_u64)"};
+                            "v_fma_f64", "v_mad_u32_u24", "v_fma_f32", "u64 add (v_lshl_add_u64)",
+                            "v_mad_u64_u32 (24 accumulators, uniform multiplier)"};
+constexpr int kRow = 24;
 
 template <int OP>
 __global__ __launch_bounds__(256) void k_op(uint64_t* out, int iters, uint32_t seed, long long* clk) {
@@ -35,7 +40,23 @@ __global__ __launch_bounds__(256) void k_op(uint64_t* out, int iters, uint32_t s
   long long c0 = 0;
   if (threadIdx.x == 0) c0 = __builtin_amdgcn_s_memtime();
   uint64_t acc = 0;
-  if constexpr (OP == FMA_F64) {
+  if constexpr (OP == MAD_ROW) {
+    uint64_t T[kRow];
+    uint32_t a[kRow];
+#pragma unroll
+    for (int j = 0; j < kRow; ++j) {
+      T[j] = (uint64_t)t * (j + 5);
+      a[j] = (t * 2654435761u + j) & 0x0FFFFFFFu;
+    }
+    uint32_t b = seed & 0x0FFFFFFFu;
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+      for (int j = 0; j < kRow; ++j) T[j] = (uint64_t)a[j] * b + T[j];
+      b = (b * 1664525u + 1013904223u) & 0x0FFFFFFFu;   // uniform: stays in an SGPR
+    }
+#pragma unroll
+    for (int j = 0; j < kRow; ++j) acc += T[j];
+  } else if constexpr (OP == FMA_F64) {
     double d[kChains];
     const double m = 0.9999999, a = 1e-7 * (double)(t & 7);
 #pragma unroll
@@ -108,7 +129,7 @@ void run(int cus, int iters, uint64_t* out, long long* clk) {
   CHECK(hipEventElapsedTime(&ms, e0, e1));
   long long ticks = 0;
   CHECK(hipMemcpy(&ticks, clk, sizeof(ticks), hipMemcpyDeviceToHost));
-  const double lane_ops = (double)grid * 256 * iters * kChains;
+  const double lane_ops = (double)grid * 256 * iters * (OP == MAD_ROW ? kRow : kChains);
   const double per_s = lane_ops / (ms * 1e-3);
   // s_memtime runs at a fixed 100 MHz reference on CDNA; report ops per CU per 2.4 GHz clock too
   const double per_clk_cu = per_s / cus / 2.4e9;
@@ -137,6 +158,7 @@ int main(int argc, char** argv) {
   run<MAD_U32_U24>(cus, iters, out, clk);
   run<FMA_F32>(cus, iters, out, clk);
   run<LSHL_ADD_U64>(cus, iters, out, clk);
+  run<MAD_ROW>(cus, iters, out, clk);
   CHECK(hipFree(out));
   CHECK(hipFree(clk));
   return 0;
