@@ -204,6 +204,101 @@ __global__ __launch_bounds__(kSlBlock) SL_OCC void k_fbpowm(Key k, const uint32_
   store_slice<C>(out + i * L, g, acc);
 }
 
+// hs^(a') mod n^2 through the radix-2^28 table (same lookup order as fbpowm_mont), result in
+// NORMAL form as this lane's C 32-bit words. Scratch: B (entry / conversion, L28 words per element).
+template <int C, int G>
+__device__ __forceinline__ void fbpowm28(uint32_t (&out)[C], const Key& k, const uint32_t* A, uint32_t* B, int E,
+                                         int words, int g) {
+  constexpr int L = C * G;
+  constexpr int C28 = s28::limbs_per_lane(L, G), L28 = C28 * G;
+  const int gs = k.d.group_size;
+  int size = 0;
+  for (int w = words - 1; w >= 0; --w) {
+    const uint32_t v = A[w * E];
+    if (v) { size = w * 32 + 32 - __clz(v); break; }
+  }
+  uint32_t m28[C28], acc[C28];
+  slice_uniform<C28>(m28, k.at(k.d.off_n2_28), g);
+  slice_uniform<C28>(acc, k.at(k.d.off_n2_one28), g);
+  const uint32_t minv28 = k.d.n2_minv28;
+  const uint32_t* table = k.at(k.d.off_table28);
+  const int cols = k.d.table_cols;
+  for (int s = 0, row = 0; s < size; s += gs, ++row) {
+    const int w = size - s < gs ? size - s : gs;
+    uint32_t idx = 0;
+    for (int j = 0; j < w; ++j) {
+      const int b = s + j;
+      idx = (idx << 1) | ((A[(b >> 5) * E] >> (b & 31)) & 1u);
+    }
+    if (idx) {
+      const uint32_t* ent = table + ((int64_t)row * cols + (idx - 1)) * L28 + g * C28;
+#pragma unroll
+      for (int j = 0; j < C28; ++j) B[(g * C28 + j) * E] = ent[j];
+      lds_sync();
+      s28::mont_mul<C28, G>(acc, LdsElem{B, E}, m28, minv28, g);
+      lds_sync();
+    }
+  }
+  s28::mont_mul<C28, G>(acc, Unit{}, m28, minv28, g);   // hs^(a') mod n^2 (< n^2)
+  lds_sync();
+  to_lds<C28>(B, E, g, acc);
+  lds_sync();
+  s28::to_words<C>(out, B, E, L28, g);
+  lds_sync();
+}
+
+// PaillierEncrypt with fresh randomness through the radix-2^28 table: c = g(m) * hs^(a') mod n^2
+template <int C, int G>
+__global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_encrypt28(Key k, const long long* __restrict__ m,
+                                                                          uint32_t* __restrict__ out, long long N,
+                                                                          uint64_t seed, long long ctr0) {
+  constexpr int L = C * G, E = kSlBlock / G;
+  constexpr int L28 = s28::limbs_per_lane(L, G) * G;
+  extern __shared__ uint32_t lds[];
+  SL_ELEMENT(E, G)
+  if (i >= N) return;
+  const int words = (k.d.a_bits + 31) >> 5;
+  uint32_t* B = lds + e;
+  uint32_t* A = lds + L28 * E + e;
+  draw_a<G>(A, E, words, k.d.a_bits, seed, (uint64_t)(ctr0 + i), g);
+  lds_sync();
+  uint32_t h[C];
+  fbpowm28<C, G>(h, k, A, B, E, words, g);
+  asm volatile("" ::: "memory");
+  uint32_t n2[C], c[C];
+  slice_uniform<C>(n2, k.at(k.d.off_n2), g);
+  const uint32_t minv = k.d.n2_minv;
+  to_lds<C>(B, E, g, h);
+  make_g<C, G>(c, m[i], k, n2, g);
+  lds_sync();
+  mont_mul<C, G>(c, LdsElem{B, E}, n2, minv, g);                   // g hsa R^-1
+  mont_mul<C, G>(c, Uniform{k.at(k.d.off_n2_r2)}, n2, minv, g);   // g hsa
+  store_slice<C>(out + i * L, g, c);
+}
+
+template <int C, int G>
+__global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_fbpowm28(Key k, const uint32_t* __restrict__ a_in,
+                                                                         uint32_t* __restrict__ out, long long N,
+                                                                         uint64_t seed, long long ctr0) {
+  constexpr int L = C * G, E = kSlBlock / G;
+  constexpr int L28 = s28::limbs_per_lane(L, G) * G;
+  extern __shared__ uint32_t lds[];
+  SL_ELEMENT(E, G)
+  if (i >= N) return;
+  const int words = (k.d.a_bits + 31) >> 5;
+  uint32_t* B = lds + e;
+  uint32_t* A = lds + L28 * E + e;
+  if (a_in) {
+    for (int w = g; w < words; w += G) A[w * E] = a_in[i * words + w];
+  } else {
+    draw_a<G>(A, E, words, k.d.a_bits, seed, (uint64_t)(ctr0 + i), g);
+  }
+  lds_sync();
+  uint32_t h[C];
+  fbpowm28<C, G>(h, k, A, B, E, words, g);
+  store_slice<C>(out + i * L, g, h);
+}
+
 template <int C, int G>
 __global__ __launch_bounds__(kSlBlock) SL_OCC void k_add(Key k, const uint32_t* __restrict__ x,
                                                   const uint32_t* __restrict__ y, uint32_t* __restrict__ out,
@@ -512,6 +607,22 @@ hipError_t run_fbpowm(const Key& k, const uint32_t* a, uint32_t* out, long long 
   return hipGetLastError();
 }
 template <int C, int G>
+hipError_t run_encrypt28(const Key& k, const long long* m, uint32_t* out, long long N, uint64_t seed, long long ctr0,
+                         hipStream_t s) {
+  const int aw = (k.d.a_bits + 31) / 32;
+  const size_t lds = (size_t)(s28::limbs_per_lane(C * G, G) * G + aw) * (kSlBlock / G) * 4;
+  hipLaunchKernelGGL((k_encrypt28<C, G>), dim3(grid_of(N, G)), dim3(kSlBlock), lds, s, k, m, out, N, seed, ctr0);
+  return hipGetLastError();
+}
+template <int C, int G>
+hipError_t run_fbpowm28(const Key& k, const uint32_t* a, uint32_t* out, long long N, uint64_t seed, long long ctr0,
+                        hipStream_t s) {
+  const int aw = (k.d.a_bits + 31) / 32;
+  const size_t lds = (size_t)(s28::limbs_per_lane(C * G, G) * G + aw) * (kSlBlock / G) * 4;
+  hipLaunchKernelGGL((k_fbpowm28<C, G>), dim3(grid_of(N, G)), dim3(kSlBlock), lds, s, k, a, out, N, seed, ctr0);
+  return hipGetLastError();
+}
+template <int C, int G>
 hipError_t run_add(const Key& k, const uint32_t* x, const uint32_t* y, uint32_t* out, long long N, hipStream_t s) {
   hipLaunchKernelGGL((k_add<C, G>), dim3(grid_of(N, G)), dim3(kSlBlock), (size_t)(C * G) * (kSlBlock / G) * 4, s, k, x, y, out, N);
   return hipGetLastError();
@@ -568,12 +679,25 @@ bool sliced_available(int L, int C) {
     default: return hipErrorInvalidValue;                    \
   }
 
+// the radix-2^28 table (include/efl_hip.h off_table28) serves a family whose lane count it was built for
+inline bool table28_for(const Key& k, int C) {
+  const int G = 2 * k.d.ln / C;
+  return k.d.off_table28 >= 0 && (1 << k.d.table28_log2g) == G &&
+         k.d.n2_28_len == s28::limbs_per_lane(2 * k.d.ln, G) * G;
+}
+
 hipError_t sl_encrypt(const Key& k, int C, const long long* m, const uint32_t* hsa, uint32_t* out, long long N,
                       uint64_t seed, long long ctr0, hipStream_t s) {
+  if (!hsa && table28_for(k, C)) {
+    SL_DISPATCH(2 * k.d.ln, C, (run_encrypt28<CC, GG>(k, m, out, N, seed, ctr0, s)))
+  }
   SL_DISPATCH(2 * k.d.ln, C, (run_encrypt<CC, GG>(k, m, hsa, out, N, seed, ctr0, s)))
 }
 hipError_t sl_fbpowm(const Key& k, int C, const uint32_t* a, uint32_t* out, long long N, uint64_t seed,
                      long long ctr0, hipStream_t s) {
+  if (table28_for(k, C)) {
+    SL_DISPATCH(2 * k.d.ln, C, (run_fbpowm28<CC, GG>(k, a, out, N, seed, ctr0, s)))
+  }
   SL_DISPATCH(2 * k.d.ln, C, (run_fbpowm<CC, GG>(k, a, out, N, seed, ctr0, s)))
 }
 hipError_t sl_add(const Key& k, int C, const uint32_t* x, const uint32_t* y, uint32_t* out, long long N,

@@ -41,7 +41,9 @@ class PlKey(ctypes.Structure):
                                                "off_hq", "off_qinvp")] + \
                [("p2_28_len", ctypes.c_int32), ("p2_minv28", ctypes.c_uint32), ("q2_minv28", ctypes.c_uint32),
                 ("off_p2_28", ctypes.c_int64), ("off_q2_28", ctypes.c_int64),
-                ("off_p2_r2_28", ctypes.c_int64 * 6), ("off_q2_r2_28", ctypes.c_int64 * 6)]
+                ("off_p2_r2_28", ctypes.c_int64 * 6), ("off_q2_r2_28", ctypes.c_int64 * 6),
+                ("n2_28_len", ctypes.c_int32), ("table28_log2g", ctypes.c_int32), ("n2_minv28", ctypes.c_uint32),
+                ("off_n2_28", ctypes.c_int64), ("off_n2_one28", ctypes.c_int64), ("off_table28", ctypes.c_int64)]
 
 
 _PK = ctypes.POINTER(PlKey)
@@ -86,6 +88,18 @@ SLICINGS = {16: ([0, 8, 16, 32], [0, 8]), 32: ([0, 8, 16, 32], [0, 8, 16, 32]), 
 
 _LIMB_CLASSES = (16, 32, 64, 128)
 MAX_TABLE_BITS = 1 << 40      # gmp_utils.h:20 FBPOWM_MAX_TABLE_MEM, compared against entries x bits
+TABLE28_MAX_BYTES = 1 << 30   # above this the radix-2^28 copy of the fixed-base table is not built
+
+
+def _limbs28_rows(vals, L: int, nbytes: int) -> np.ndarray:
+    """Many ints -> [len(vals), L] radix-2^28 limbs (vectorised through the little-endian bits)."""
+    raw = np.frombuffer(b"".join(v.to_bytes(nbytes, "little") for v in vals), dtype=np.uint8)
+    bits = np.unpackbits(raw.reshape(len(vals), nbytes), axis=1, bitorder="little")
+    need = 28 * L
+    if bits.shape[1] < need:
+        bits = np.pad(bits, ((0, 0), (0, need - bits.shape[1])))
+    w = (1 << np.arange(28, dtype=np.uint32)).astype(np.uint32)
+    return (bits[:, :need].reshape(len(vals), L, 28).astype(np.uint32) * w).sum(axis=2, dtype=np.uint32)
 
 
 def _limbs(x: int, L: int) -> np.ndarray:
@@ -268,6 +282,19 @@ class KeyBlock:
         if rows * cols * n2.bit_length() > MAX_TABLE_BITS:
             raise errors.ResourceExhaustedError("Memory usage exceeds a predefined threshold.")
         d.table_rows, d.table_cols = rows, cols
+        # radix-2^28 copy for the sliced family the n^2 kernels use (include/efl_hip.h)
+        d.off_table28 = -1
+        fam = kernel_slicing(ln, False)
+        tab28 = None
+        if fam:
+            G = 2 * ln // fam
+            L28 = limbs28_total(2 * ln, G)
+            if rows * cols * L28 * 4 <= TABLE28_MAX_BYTES:
+                R28 = 1 << (28 * L28)
+                nb28 = (28 * L28 + 7) // 8
+                d.n2_28_len, d.table28_log2g = L28, G.bit_length() - 1
+                d.n2_minv28 = (-pow(n2, -1, 1 << 28)) % (1 << 28)
+                tab28 = np.empty((rows, cols, L28), dtype="<u4")
         d.off_table = pos[0]
         entry = hs % n2
         row = []
@@ -283,8 +310,20 @@ class KeyBlock:
                 row = [pow(v, sq, n2) for v in row]
             buf = b"".join((v * Rc % n2).to_bytes(nbytes, "little") for v in row)
             tab[i] = np.frombuffer(buf, dtype="<u4").reshape(cols, self.lc)
+            if tab28 is not None:
+                tab28[i] = _limbs28_rows([v * R28 % n2 for v in row], L28, nb28)
         words.append(tab.reshape(-1))
         pos[0] += tab.size
+        if tab28 is not None:
+            d.off_n2_28 = pos[0]
+            words.append(_limbs28(n2, L28))
+            pos[0] += L28
+            d.off_n2_one28 = pos[0]
+            words.append(_limbs28(R28 % n2, L28))
+            pos[0] += L28
+            d.off_table28 = pos[0]
+            words.append(tab28.reshape(-1))
+            pos[0] += tab28.size
         host = np.concatenate(words)
         self.block = torch.from_numpy(host.view(np.int32)).to(self.device)
         self.ptr = self.block.data_ptr()

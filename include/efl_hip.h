@@ -164,6 +164,17 @@ typedef struct {
   uint32_t p2_minv28, q2_minv28;
   int64_t off_p2_28, off_q2_28;
   int64_t off_p2_r2_28[6], off_q2_r2_28[6];
+  /* Radix-2^28 fixed-base table for the sliced n^2 kernels that spread n^2 over
+   * G = 2^table28_log2g lanes (the family chosen when the key was set):
+   *   n2_28_len     L28 = G * ceil(ceil((64 ln + 2) / 28) / G) limbs
+   *   off_n2_28     n^2 as L28 28-bit limbs; n2_minv28 = -n^2^-1 mod 2^28
+   *   off_n2_one28  R28 mod n^2, R28 = 2^(28 L28)
+   *   off_table28   table_rows x table_cols entries of L28 limbs, entry [i][j] =
+   *                 hs^((j+1) 2^(group_size i)) R28 mod n^2; -1 when absent (other families, or a
+   *                 table too large to hold twice), and the 32-bit table serves. */
+  int32_t n2_28_len, table28_log2g;
+  uint32_t n2_minv28;
+  int64_t off_n2_28, off_n2_one28, off_table28;
 } efl_pl_key;
 
 /*
