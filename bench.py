@@ -189,6 +189,8 @@ def stage_p(args):
             if name == "decrypt" and fam:     # sliced decryption exponentiates in radix 2^28
                 L28 = pc.limbs28_total(k.ln, k.ln // fam)
                 issued = sum(_mont_macs(L28, e.bit_length() - 1, bin(e).count("1") - 1) for e in (pm1, qm1))
+            if name == "encrypt" and k.desc.off_table28 >= 0:   # the radix-2^28 table serves encryption
+                issued = _mont_macs(k.desc.n2_28_len, 0, rows * (1 - 2.0 ** -g) + 1)
             res[name] = {"elements_per_s": round(per_s), "ms": round(times[name] * 1e3, 3),
                          "macs_per_element": int(macs),
                          "roofline": {"bound": "valu", "achieved": round(per_s * macs / 1e12, 3),
@@ -207,7 +209,124 @@ def stage_p(args):
             out["cpu_baseline"] = stage_p_cpu(n_bytes, a_bytes, g, p, q, hs, args.cpu_threads, cpu_keys)
             for name in ("encrypt", "decrypt"):
                 out[name]["vs_cpu"] = round(out[name]["elements_per_s"] / out["cpu_baseline"][name], 1)
+        if "MNIST" in label:
+            out["matmul"] = stage_p_matmul(args, efl, pc, kp, lib, sh, stream, dev)
         print(json.dumps(out), flush=True)
+
+
+# the receiver's forward product of the paillier_mnist example (paillier_layer.py:136:
+# x @ fixedpoint_encode(w, decrease_precision=True)): x [256, 28*14] encrypted by the sender
+# (leader_dense.py:44 / follower_dense.py:23 batch 256), w [392, 128] glorot-uniform
+STAGE_P_MATMUL = (256, 392, 128)
+
+
+def stage_p_matmul(args, efl, pc, kp, lib, sh, stream, dev):
+    """PaillierMatmul (paillier.cc:941-1051) on the MNIST receiver shape: the efl_pl_matmul kernel
+    (all u*w outputs, every term's x^|y| and 2^(exponent - min) squarings, both sign products) timed
+    with HIP events; the plaintext of the first outputs checked exactly after the caller's
+    invert + add finish."""
+    u, v, w = STAGE_P_MATMUL
+    k = kp.key
+    gen = torch.Generator(device=dev).manual_seed(3)
+    x = torch.randn(u, v, device=dev, generator=gen)
+    lim = (6.0 / (v + w)) ** 0.5
+    W = (torch.rand(v, w, device=dev, generator=gen) * 2 - 1) * lim
+    xm, xe = efl.lib.convert_to_fixed_point(x)
+    ym, ye = efl.lib.convert_to_fixed_point(W, decrease_precision=True)
+    X = torch.empty((u * v, k.lc), dtype=torch.int32, device=dev)
+    efl.lib.check(lib.efl_pl_encrypt(*k.args(), xm.data_ptr(), None, X.data_ptr(), u * v, 11, 0, sh))
+    zpos = torch.empty((u * w, k.lc), dtype=torch.int32, device=dev)
+    zneg = torch.empty_like(zpos)
+    ze = torch.empty((u, w), dtype=torch.int64, device=dev)
+
+    def mm():
+        efl.lib.check(lib.efl_pl_matmul(*k.args(), X.data_ptr(), xe.data_ptr(), ym.data_ptr(), ye.data_ptr(),
+                                        zpos.data_ptr(), zneg.data_ptr(), ze.data_ptr(), u, v, w, sh))
+
+    mm()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 3
+    e0.record(stream)
+    for _ in range(reps):
+        mm()
+    e1.record(stream)
+    e1.synchronize()
+    t = e0.elapsed_time(e1) / reps * 1e-3
+    # Montgomery products the kernel executes, counted from the data (per group, ignoring lanes a
+    # wave masks off): x R once per x element; per output and sign, Straus over the terms of that
+    # sign: (top level - 1) shared squarings, popcount(|y|) multiplies per term less the first (a
+    # copy), one conversion out. `per_term_products` is one square-and-multiply per term instead
+    # (bits-1 + popcount-1 + d, a conversion in and a multiply into the product), the schedule the
+    # reference's powm-per-term loop (paillier.cc:1015-1032) has.
+    xe_h, ym_h, ye_h = (a.cpu().numpy().astype(np.int64) for a in (xe, ym, ye))
+    ex = xe_h[:, :, None] + ye_h[None, :, :]                  # [u, v, w]
+    d = ex - ex.min(axis=1, keepdims=True)
+    nz = ym_h != 0
+    ay = np.abs(ym_h)
+    bits = np.zeros(ym_h.shape, dtype=np.int64)
+    pop = np.zeros(ym_h.shape, dtype=np.int64)
+    for q in range(63):
+        hit = (ay >> q) & 1
+        pop += hit
+        bits = np.where(hit == 1, q + 1, bits)
+    products = u * v
+    for mask in (nz & (ym_h > 0), nz & (ym_h < 0)):
+        top = np.where(mask[None, :, :], d + bits[None, :, :], 0).max(axis=1)    # [u, w]
+        started = mask.any(axis=0)[None, :].repeat(u, axis=0)
+        products += int(np.maximum(top - 1, 0)[started].sum()) + u * int(pop[mask].sum()) - int(started.sum())
+        products += int(started.sum())
+    per_term = u * int((bits + pop)[nz].sum()) + int((d * nz[None, :, :]).sum()) + 2 * u * w
+    L = k.lc
+    fam = pc.kernel_slicing(k.ln, False)
+    L_issued = k.desc.n2_28_len if (fam and k.desc.off_table28 >= 0) else L
+    macs, issued = 2 * L * L * products, 2 * L_issued * L_issued * products
+    # plaintext check of the first outputs: sum_j xm*ym*2^(xe+ye-min), exactly
+    zm, zexp = kp.matmul(pc.CipherTensor(X, (u, v), k), xe, ym, ye)
+    n_chk = 64
+    dec = kp.decrypt(pc.CipherTensor(zm.limbs[:n_chk], (n_chk,), k), dtype="string").to_ints()
+    xm_h = xm.cpu().numpy()
+    ze_h = zexp.cpu().numpy().reshape(-1)
+    for o in range(n_chk):
+        i, q = divmod(o, w)
+        want = sum((int(xm_h[i, j]) * int(ym_h[j, q])) << int(ex[i, j, q] - ze_h[o]) for j in range(v))
+        if dec[o] != want:
+            raise SystemExit(f"bench: PaillierMatmul output {o} is wrong")
+    res = {"shape": [u, v, w], "outputs_per_s": round(u * w / t, 1), "ms": round(t * 1e3, 3),
+           "montgomery_products_per_output": round(products / (u * w), 1),
+           "per_term_products_per_output": round(per_term / (u * w), 1),
+           "roofline": {"bound": "valu", "achieved": round(macs / t / 1e12, 3),
+                        "peak": round(MAD_U64_U32_PEAK / 1e12, 3), "unit": "TMAC/s",
+                        "frac": round(macs / t / MAD_U64_U32_PEAK, 4),
+                        "limb_products_per_s": round(issued / t / 1e12, 3),
+                        "issue_frac": round(issued / t / MAD_U64_U32_PEAK, 4)},
+           "kernel_family": fam, "cpu_baseline": None}
+    if not args.no_cpu_baseline:
+        res["cpu_baseline"] = stage_p_matmul_cpu(kp, xe_h, ym_h, ye_h, v, w, args.cpu_threads)
+        res["vs_cpu"] = round(res["outputs_per_s"] / res["cpu_baseline"]["value"], 1)
+    return res
+
+
+def stage_p_matmul_cpu(kp, xe, ym, ye, v, w, threads):
+    """The reference's PaillierMatmul compute (oracle/paillier_gmp.c pl_gmp_matmul_bench) on the
+    first rows of the same exponents and weights, sized for a few seconds on `threads` threads."""
+    import ctypes
+    from oracle import fxp, paillier as P
+    L = fxp.lib()
+    L.pl_gmp_matmul_bench.argtypes = [ctypes.c_char_p] + [ctypes.c_void_p] * 3 + [ctypes.c_int] * 4 + \
+        [ctypes.POINTER(ctypes.c_double)]
+    n_hex = P.hx(kp.key.n).encode()
+    t = (ctypes.c_double * 2)()
+    ym_c, ye_c = np.ascontiguousarray(ym), np.ascontiguousarray(ye)
+    rows = 1
+    while True:
+        xe_c = np.ascontiguousarray(xe[:rows])
+        L.pl_gmp_matmul_bench(n_hex, xe_c.ctypes.data, ym_c.ctypes.data, ye_c.ctypes.data, rows, v, w, threads, t)
+        if t[0] + t[1] > 2.0 or rows >= xe.shape[0]:
+            break
+        rows = min(xe.shape[0], rows * max(2, int(3.0 / max(t[0] + t[1], 1e-3))))
+    return {"value": round(rows * w / (t[0] + t[1]), 1), "unit": "outputs/s", "cores": threads, "kind": "port",
+            "sample": f"{rows} rows x {w} outputs ({rows * v} ciphertext inversions, serial as paillier.cc:994-999, "
+                      f"then GMP powm per term over {threads} threads)"}
 
 
 def stage_p_cpu(n_bytes, a_bytes, g, p, q, hs, threads, cache):

@@ -583,9 +583,11 @@ __global__ __launch_bounds__(kPlBlock) void k_matmul(Key k, const uint32_t* __re
   uint32_t* acol = lds + threadIdx.x;
   uint32_t* bcol = lds + LC * S + threadIdx.x;
   uint32_t* pcol = lds + 2 * LC * S + threadIdx.x;   // running positive product (Montgomery)
-  const long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (o >= (long long)u * w) return;
-  const int i = (int)(o / w), kk = (int)(o % w);
+  const long long lin = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (lin >= (long long)u * w) return;
+  // column by column: the lanes of a wave share every term's |y| (no divergence in x^|y|)
+  const int i = (int)(lin % u), kk = (int)(lin / u);
+  const long long o = (long long)i * w + kk;
   const uint32_t* n2 = k.at(k.d.off_n2);
   const uint32_t* one = k.at(k.d.off_n2_one);
   long long mn = 0x7FFFFFFFFFFFFFFFll;

@@ -355,6 +355,204 @@ __global__ __launch_bounds__(kSlBlock) SL_OCC void k_powm(Key k, const uint32_t*
   store_slice<C>(out + i * L, g, t);
 }
 
+// ---- radix-2^28 variants of powm / matmul (the family the radix-2^28 table was built for) ----
+
+// this lane's 28-bit slice of x R28 mod n^2 from x in normal form (32-bit words in HBM); SCR scratch
+template <int C, int G>
+__device__ __forceinline__ void to_mont28(uint32_t (&t)[s28::limbs_per_lane(C * G, G)], const uint32_t* x,
+                                          const Key& k, const uint32_t (&m28)[s28::limbs_per_lane(C * G, G)],
+                                          uint32_t* SCR, int E, int g) {
+  constexpr int L = C * G, C28 = s28::limbs_per_lane(L, G);
+  uint32_t w[C];
+  load_slice<C>(w, x, g);
+  lds_sync();
+  to_lds<C>(SCR, E, g, w);
+  lds_sync();
+  s28::from_words<C28>(t, SCR, E, L, g);
+  lds_sync();
+  s28::mont_mul<C28, G>(t, Uniform{k.at(k.d.off_n2_r2_28)}, m28, k.d.n2_minv28, g);
+}
+
+// normal form (< n^2) from a radix-2^28 Montgomery slice, stored as 32-bit words
+template <int C, int G>
+__device__ __forceinline__ void store_from_mont28(uint32_t* out, uint32_t (&t)[s28::limbs_per_lane(C * G, G)],
+                                                  const uint32_t (&m28)[s28::limbs_per_lane(C * G, G)],
+                                                  uint32_t minv28, uint32_t* SCR, int E, int g) {
+  constexpr int L = C * G, C28 = s28::limbs_per_lane(L, G), L28 = C28 * G;
+  s28::mont_mul<C28, G>(t, Unit{}, m28, minv28, g);
+  lds_sync();
+  to_lds<C28>(SCR, E, g, t);
+  lds_sync();
+  uint32_t w[C];
+  s28::to_words<C>(w, SCR, E, L28, g);
+  store_slice<C>(out, g, w);
+}
+
+template <int C, int G>
+__global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_powm28(Key k, const uint32_t* __restrict__ x,
+                                                                       const uint32_t* __restrict__ exps, int ewords,
+                                                                       uint32_t* __restrict__ out, long long N) {
+  constexpr int L = C * G, E = kSlBlock / G;
+  constexpr int C28 = s28::limbs_per_lane(L, G), L28 = C28 * G;
+  extern __shared__ uint32_t lds[];
+  SL_ELEMENT(E, G)
+  if (i >= N) return;
+  uint32_t* BASE = lds + e;
+  uint32_t* SCR = lds + L28 * E + e;
+  const uint32_t* ex = exps + i * ewords;
+  int ebits = 0;
+  for (int w = ewords - 1; w >= 0; --w)
+    if (ex[w]) { ebits = w * 32 + 32 - __clz(ex[w]); break; }
+  if (ebits == 0) {
+    uint32_t one[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) one[j] = (g == 0 && j == 0) ? 1u : 0u;
+    store_slice<C>(out + i * L, g, one);
+    return;
+  }
+  uint32_t m28[C28], t[C28];
+  slice_uniform<C28>(m28, k.at(k.d.off_n2_28), g);
+  const uint32_t minv28 = k.d.n2_minv28;
+  to_mont28<C, G>(t, x + i * L, k, m28, SCR, E, g);
+  lds_sync();
+  to_lds<C28>(BASE, E, g, t);
+#pragma unroll 1
+  for (int b = ebits - 2; b >= 0; --b) {
+    s28::mont_sqr<C28, G>(t, SCR, E, m28, minv28, g);
+    if ((ex[b >> 5] >> (b & 31)) & 1u) s28::mont_mul<C28, G>(t, LdsElem{BASE, E}, m28, minv28, g);
+  }
+  store_from_mont28<C, G>(out + i * L, t, m28, minv28, SCR, E, g);
+}
+
+// ---- PaillierMatmul in radix 2^28: x converted once, then one multi-exponentiation per output ----
+//
+// Output (i, k) is prod_j x_ij^(|y_jk| 2^(d_ijk)) over the terms of each sign, d = xe + ye - min.
+// Instead of one square-and-multiply per term (bits(|y|) - 1 + d squarings each), the terms of
+// one sign share the squarings (Straus): from the top bit level down, square the product once,
+// then multiply in every x_ij whose exponent has that bit. Squarings drop from sum_j (bits + d) to
+// max_j (bits + d) per sign; multiplies stay popcount(|y|) per term. x_ij R (radix 2^28) is
+// computed once per x element (k_tomont28) instead of once per output, and read from HBM as the
+// register operand of the multiply; the two running products are the LDS operand.
+//
+// Groups walk the outputs column by column (consecutive groups: consecutive rows, the same column
+// of y), so the groups of a wave share every term's |y| and differ only through d.
+
+// padded radix-2^28 slice of one element in HBM: lane g's C28 limbs at [g * CP, g * CP + C28)
+template <int C28>
+constexpr int pad4() { return (C28 + 3) & ~3; }
+
+template <int C, int G>
+__global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_tomont28(Key k, const uint32_t* __restrict__ X,
+                                                                         uint32_t* __restrict__ Xm, long long N) {
+  constexpr int L = C * G, E = kSlBlock / G;
+  constexpr int C28 = s28::limbs_per_lane(L, G), CP = pad4<C28>();
+  extern __shared__ uint32_t lds[];
+  SL_ELEMENT(E, G)
+  if (i >= N) return;
+  uint32_t m28[C28], t[C28];
+  slice_uniform<C28>(m28, k.at(k.d.off_n2_28), g);
+  to_mont28<C, G>(t, X + i * L, k, m28, lds + e, E, g);
+  uint32_t* q = Xm + i * (long long)(CP * G) + g * CP;
+#pragma unroll
+  for (int j = 0; j < CP; j += 4)
+    *reinterpret_cast<uint4*>(q + j) = make_uint4(t[j], j + 1 < C28 ? t[j + 1] : 0u, j + 2 < C28 ? t[j + 2] : 0u,
+                                                  j + 3 < C28 ? t[j + 3] : 0u);
+}
+
+template <int C28>
+__device__ __forceinline__ void load28(uint32_t (&t)[C28], const uint32_t* __restrict__ q) {
+  constexpr int CP = pad4<C28>();
+#pragma unroll
+  for (int j = 0; j < CP; j += 4) {
+    const uint4 v = *reinterpret_cast<const uint4*>(q + j);
+    t[j] = v.x;
+    if (j + 1 < C28) t[j + 1] = v.y;
+    if (j + 2 < C28) t[j + 2] = v.z;
+    if (j + 3 < C28) t[j + 3] = v.w;
+  }
+}
+
+template <int C, int G>
+__global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_matmul28(
+    Key k, const uint32_t* __restrict__ Xm, const long long* __restrict__ xe, const long long* __restrict__ ym,
+    const long long* __restrict__ ye, uint32_t* __restrict__ zpos, uint32_t* __restrict__ zneg,
+    long long* __restrict__ ze, int u, int v, int w) {
+  constexpr int L = C * G, E = kSlBlock / G;
+  constexpr int C28 = s28::limbs_per_lane(L, G), L28 = C28 * G, CP = pad4<C28>();
+  extern __shared__ uint32_t lds[];
+  SL_ELEMENT(E, G)
+  if (i >= (long long)u * w) return;
+  const int row = (int)(i % u), kk = (int)(i / u);
+  const long long o = (long long)row * w + kk;
+  uint32_t* ACC[2] = {lds + e, lds + L28 * E + e};   // running products: y > 0, y < 0
+  uint32_t m28[C28], t[C28];
+  slice_uniform<C28>(m28, k.at(k.d.off_n2_28), g);
+  const uint32_t minv28 = k.d.n2_minv28;
+  const long long* xr = xe + (long long)row * v;
+  const long long* yc = ym + kk;
+  const long long* ec = ye + kk;
+  long long mn = 0x7FFFFFFFFFFFFFFFll;
+  for (int j = 0; j < v; ++j) {
+    const long long ex = xr[j] + ec[(long long)j * w];
+    mn = ex < mn ? ex : mn;
+  }
+  // top bit level of any term's exponent |y| 2^d
+  long long top = 0;
+  for (int j = 0; j < v; ++j) {
+    const long long y = yc[(long long)j * w];
+    if (y == 0) continue;
+    const uint64_t ay = y < 0 ? 0ull - (uint64_t)y : (uint64_t)y;
+    const long long lvl = xr[j] + ec[(long long)j * w] - mn + (64 - __clzll((long long)ay));
+    top = lvl > top ? lvl : top;
+  }
+  bool started0 = false, started1 = false;   // products still 1 skip their squarings
+  for (long long b = top - 1; b >= 0; --b) {
+#pragma unroll
+    for (int sgn = 0; sgn < 2; ++sgn) {
+      if (!(sgn ? started1 : started0)) continue;
+      from_lds<C28>(t, ACC[sgn], E, g);
+      s28::mont_mul<C28, G>(t, LdsElem{ACC[sgn], E}, m28, minv28, g);
+      lds_sync();
+      to_lds<C28>(ACC[sgn], E, g, t);
+      lds_sync();
+    }
+    for (int j = 0; j < v; ++j) {
+      const long long y = yc[(long long)j * w];
+      const long long p = b - (xr[j] + ec[(long long)j * w] - mn);
+      if (y == 0 || p < 0 || p >= 64) continue;
+      const uint64_t ay = y < 0 ? 0ull - (uint64_t)y : (uint64_t)y;
+      if (!((ay >> p) & 1ull)) continue;
+      const bool neg = y < 0;
+      uint32_t* acc = neg ? ACC[1] : ACC[0];
+      load28<C28>(t, Xm + ((long long)row * v + j) * (CP * G) + g * CP);
+      if (neg ? started1 : started0) {
+        s28::mont_mul<C28, G>(t, LdsElem{acc, E}, m28, minv28, g);
+        lds_sync();
+      }
+      to_lds<C28>(acc, E, g, t);
+      lds_sync();
+      if (neg) started1 = true;
+      else started0 = true;
+    }
+  }
+  uint32_t* out[2] = {zpos + o * L, zneg + o * L};
+#pragma unroll
+  for (int sgn = 0; sgn < 2; ++sgn) {
+    if (sgn ? started1 : started0) {
+      from_lds<C28>(t, ACC[sgn], E, g);
+      lds_sync();
+      store_from_mont28<C, G>(out[sgn], t, m28, minv28, ACC[sgn], E, g);   // the product's LDS is the scratch
+    } else {
+      uint32_t one[C];
+#pragma unroll
+      for (int j = 0; j < C; ++j) one[j] = (g == 0 && j == 0) ? 1u : 0u;
+      store_slice<C>(out[sgn], g, one);
+    }
+    lds_sync();
+  }
+  if (g == 0) ze[o] = mn;
+}
+
 // PaillierMatmul core, one group per output (see paillier.hip k_matmul)
 template <int C, int G>
 __global__ __launch_bounds__(kSlBlock) SL_OCC void k_matmul(Key k, const uint32_t* __restrict__ X,
@@ -366,9 +564,9 @@ __global__ __launch_bounds__(kSlBlock) SL_OCC void k_matmul(Key k, const uint32_
   constexpr int L = C * G, E = kSlBlock / G;
   extern __shared__ uint32_t lds[];
   SL_ELEMENT(E, G)
-  const long long o = i;
-  if (o >= (long long)u * w) return;
-  const int row = (int)(o / w), kk = (int)(o % w);
+  if (i >= (long long)u * w) return;
+  const int row = (int)(i % u), kk = (int)(i / u);   // column by column, as k_matmul28
+  const long long o = (long long)row * w + kk;
   uint32_t* BASE = lds + e;
   uint32_t* SCR = lds + L * E + e;
   uint32_t* POS = lds + 2 * L * E + e;
@@ -623,6 +821,31 @@ hipError_t run_fbpowm28(const Key& k, const uint32_t* a, uint32_t* out, long lon
   return hipGetLastError();
 }
 template <int C, int G>
+hipError_t run_powm28(const Key& k, const uint32_t* x, const uint32_t* e, int ew, uint32_t* out, long long N,
+                      hipStream_t s) {
+  const size_t lds = (size_t)(2 * s28::limbs_per_lane(C * G, G) * G) * (kSlBlock / G) * 4;
+  hipLaunchKernelGGL((k_powm28<C, G>), dim3(grid_of(N, G)), dim3(kSlBlock), lds, s, k, x, e, ew, out, N);
+  return hipGetLastError();
+}
+template <int C, int G>
+hipError_t run_matmul28(const Key& k, const uint32_t* X, const long long* xe, const long long* ym, const long long* ye,
+                        uint32_t* zpos, uint32_t* zneg, long long* ze, int u, int v, int w, hipStream_t s) {
+  constexpr int C28 = s28::limbs_per_lane(C * G, G), L28 = C28 * G, E = kSlBlock / G;
+  const long long nx = (long long)u * v;
+  uint32_t* Xm = nullptr;   // x R mod n^2 in padded radix-2^28 slices, stream-ordered scratch
+  hipError_t err = hipMallocAsync(reinterpret_cast<void**>(&Xm), (size_t)nx * pad4<C28>() * G * 4, s);
+  if (err != hipSuccess) return err;
+  hipLaunchKernelGGL((k_tomont28<C, G>), dim3(grid_of(nx, G)), dim3(kSlBlock), (size_t)L28 * E * 4, s, k, X, Xm, nx);
+  err = hipGetLastError();
+  if (err == hipSuccess) {
+    hipLaunchKernelGGL((k_matmul28<C, G>), dim3(grid_of((long long)u * w, G)), dim3(kSlBlock),
+                       (size_t)2 * L28 * E * 4, s, k, Xm, xe, ym, ye, zpos, zneg, ze, u, v, w);
+    err = hipGetLastError();
+  }
+  const hipError_t ferr = hipFreeAsync(Xm, s);
+  return err != hipSuccess ? err : ferr;
+}
+template <int C, int G>
 hipError_t run_add(const Key& k, const uint32_t* x, const uint32_t* y, uint32_t* out, long long N, hipStream_t s) {
   hipLaunchKernelGGL((k_add<C, G>), dim3(grid_of(N, G)), dim3(kSlBlock), (size_t)(C * G) * (kSlBlock / G) * 4, s, k, x, y, out, N);
   return hipGetLastError();
@@ -706,11 +929,17 @@ hipError_t sl_add(const Key& k, int C, const uint32_t* x, const uint32_t* y, uin
 }
 hipError_t sl_powm(const Key& k, int C, const uint32_t* x, const uint32_t* e, int ew, uint32_t* out, long long N,
                    hipStream_t s) {
+  if (table28_for(k, C)) {
+    SL_DISPATCH(2 * k.d.ln, C, (run_powm28<CC, GG>(k, x, e, ew, out, N, s)))
+  }
   SL_DISPATCH(2 * k.d.ln, C, (run_powm<CC, GG>(k, x, e, ew, out, N, s)))
 }
 hipError_t sl_matmul(const Key& k, int C, const uint32_t* X, const long long* xe, const long long* ym,
                      const long long* ye, uint32_t* zpos, uint32_t* zneg, long long* ze, int u, int v, int w,
                      hipStream_t s) {
+  if (table28_for(k, C)) {
+    SL_DISPATCH(2 * k.d.ln, C, (run_matmul28<CC, GG>(k, X, xe, ym, ye, zpos, zneg, ze, u, v, w, s)))
+  }
   SL_DISPATCH(2 * k.d.ln, C, (run_matmul<CC, GG>(k, X, xe, ym, ye, zpos, zneg, ze, u, v, w, s)))
 }
 hipError_t sl_decrypt(const Key& k, int C, const uint32_t* ct, uint32_t* mag, signed char* neg, long long N,

@@ -43,7 +43,8 @@ class PlKey(ctypes.Structure):
                 ("off_p2_28", ctypes.c_int64), ("off_q2_28", ctypes.c_int64),
                 ("off_p2_r2_28", ctypes.c_int64 * 6), ("off_q2_r2_28", ctypes.c_int64 * 6),
                 ("n2_28_len", ctypes.c_int32), ("table28_log2g", ctypes.c_int32), ("n2_minv28", ctypes.c_uint32),
-                ("off_n2_28", ctypes.c_int64), ("off_n2_one28", ctypes.c_int64), ("off_table28", ctypes.c_int64)]
+                ("off_n2_28", ctypes.c_int64), ("off_n2_one28", ctypes.c_int64), ("off_table28", ctypes.c_int64),
+                ("off_n2_r2_28", ctypes.c_int64)]
 
 
 _PK = ctypes.POINTER(PlKey)
@@ -320,6 +321,9 @@ class KeyBlock:
             pos[0] += L28
             d.off_n2_one28 = pos[0]
             words.append(_limbs28(R28 % n2, L28))
+            pos[0] += L28
+            d.off_n2_r2_28 = pos[0]
+            words.append(_limbs28(R28 * R28 % n2, L28))
             pos[0] += L28
             d.off_table28 = pos[0]
             words.append(tab28.reshape(-1))

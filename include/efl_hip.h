@@ -171,10 +171,12 @@ typedef struct {
    *   off_n2_one28  R28 mod n^2, R28 = 2^(28 L28)
    *   off_table28   table_rows x table_cols entries of L28 limbs, entry [i][j] =
    *                 hs^((j+1) 2^(group_size i)) R28 mod n^2; -1 when absent (other families, or a
-   *                 table too large to hold twice), and the 32-bit table serves. */
+   *                 table too large to hold twice), and the 32-bit table serves; the powm and
+   *                 matmul kernels of that family then also run in 32-bit limbs. */
   int32_t n2_28_len, table28_log2g;
   uint32_t n2_minv28;
   int64_t off_n2_28, off_n2_one28, off_table28;
+  int64_t off_n2_r2_28;   /* R28^2 mod n^2 (same L28): powm and matmul of that family in radix 2^28 */
 } efl_pl_key;
 
 /*

@@ -372,3 +372,113 @@ EFL_EXPORT void pl_gmp_bench(const char* p_hex, const char* q_hex, const char* h
   mpz_clear(hs);
   mpz_clears(k.n, k.n2, k.p, k.q, k.p2, k.q2, k.hp, k.hq, k.qinv, k.mx, NULL);
 }
+
+/* ------------------------------------------------------------------------------------------
+ * CPU baseline of PaillierMatmul (bench.py --stage p, cpu_baseline leg only), restating the op's
+ * compute (paillier.cc:987-1041): every x ciphertext is inverted mod n^2 serially before the
+ * sharded loop (:994-999); each output (i, k) takes min_j(xe + ye), then per term
+ * powm(x, y) (y >= 0, x parsed from its hex string) or powm(x^-1, -y), powm by 2^(exp - min) and
+ * a multiply mod n^2 into the sum (:1015-1032), and prints the sum as hex (:1034). Outputs are
+ * split into contiguous blocks over `threads` pthreads. x: `rows * v` ciphertexts drawn uniformly
+ * below n^2 from a fixed MT seed; xe [rows][v], ym / ye [v][w] as given. times[0] = inversion
+ * seconds, times[1] = output-loop seconds (wall).
+ * ------------------------------------------------------------------------------------------ */
+typedef struct {
+  mpz_srcptr n2;
+  char** xs;
+  mpz_t* xinv;
+  const long long *xe, *ym, *ye;
+  int v, w;
+  long long lo, hi;
+} mm_job;
+
+static void* mm_worker(void* arg) {
+  mm_job* jb = (mm_job*)arg;
+  mpz_t addend, e, sum, x;
+  mpz_inits(addend, e, sum, x, NULL);
+  const int v = jb->v, w = jb->w;
+  for (long long o = jb->lo; o < jb->hi; ++o) {
+    const long long i = o / w, kk = o % w;
+    long long mn = 0x7FFFFFFFFFFFFFFFLL;
+    for (int j = 0; j < v; ++j) {
+      const long long ex = jb->xe[i * v + j] + jb->ye[(long long)j * w + kk];
+      if (ex < mn) mn = ex;
+    }
+    for (int j = 0; j < v; ++j) {
+      const long long ex = jb->xe[i * v + j] + jb->ye[(long long)j * w + kk] - mn;
+      const long long y = jb->ym[(long long)j * w + kk];
+      const unsigned long long ay = y < 0 ? 0ull - (unsigned long long)y : (unsigned long long)y;
+      mpz_import(e, 1, -1, sizeof(ay), 0, 0, &ay);
+      if (y >= 0) {
+        mpz_set_str(x, jb->xs[i * v + j], 16);
+        mpz_powm(addend, x, e, jb->n2);
+      } else {
+        mpz_powm(addend, jb->xinv[i * v + j], e, jb->n2);
+      }
+      mpz_set_ui(e, 1);
+      mpz_mul_2exp(e, e, (mp_bitcnt_t)ex);
+      mpz_powm(addend, addend, e, jb->n2);
+      if (!j) {
+        mpz_set(sum, addend);
+      } else {
+        mpz_mul(sum, addend, sum);
+        mpz_mod(sum, sum, jb->n2);
+      }
+    }
+    char* s = mpz_get_str(NULL, 16, sum);
+    void (*freefunc)(void*, size_t);
+    mp_get_memory_functions(NULL, NULL, &freefunc);
+    freefunc(s, strlen(s) + 1);
+  }
+  mpz_clears(addend, e, sum, x, NULL);
+  return NULL;
+}
+
+EFL_EXPORT void pl_gmp_matmul_bench(const char* n_hex, const long long* xe, const long long* ym,
+                                    const long long* ye, int rows, int v, int w, int threads, double* times) {
+  mpz_t n, n2, c;
+  mpz_inits(n, n2, c, NULL);
+  mpz_set_str(n, n_hex, 16);
+  mpz_mul(n2, n, n);
+  const long long nx = (long long)rows * v;
+  char** xs = (char**)calloc((size_t)nx, sizeof(char*));
+  mpz_t* xinv = (mpz_t*)malloc(sizeof(mpz_t) * (size_t)nx);
+  gmp_randstate_t st;
+  gmp_randinit_mt(st);
+  gmp_randseed_ui(st, 2024ul);
+  for (long long t = 0; t < nx; ++t) {
+    do {
+      mpz_urandomm(c, st, n2);
+    } while (mpz_sgn(c) == 0);
+    xs[t] = mpz_get_str(NULL, 16, c);
+    mpz_init(xinv[t]);
+  }
+  double t0 = now_s();
+  for (long long t = 0; t < nx; ++t) {
+    mpz_set_str(c, xs[t], 16);
+    mpz_invert(xinv[t], c, n2);
+  }
+  times[0] = now_s() - t0;
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  pthread_t th[256];
+  mm_job jobs[256];
+  const long long outs = (long long)rows * w;
+  t0 = now_s();
+  for (int t = 0; t < threads; ++t) {
+    jobs[t] = (mm_job){n2, xs, xinv, xe, ym, ye, v, w, outs * t / threads, outs * (t + 1) / threads};
+    pthread_create(&th[t], NULL, mm_worker, &jobs[t]);
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+  times[1] = now_s() - t0;
+  void (*freefunc)(void*, size_t);
+  mp_get_memory_functions(NULL, NULL, &freefunc);
+  for (long long t = 0; t < nx; ++t) {
+    freefunc(xs[t], strlen(xs[t]) + 1);
+    mpz_clear(xinv[t]);
+  }
+  free(xs);
+  free(xinv);
+  gmp_randclear(st);
+  mpz_clears(n, n2, c, NULL);
+}

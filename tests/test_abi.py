@@ -39,6 +39,24 @@ def test_library_exports_every_declared_symbol():
         assert getattr(lib, n)
 
 
+def test_pl_key_struct_matches_ctypes_mirror(tmp_path):
+    """efl_pl_key (include/efl_hip.h) and its ctypes mirror PlKey agree on size and every offset:
+    compiled with gcc from the header, so a field added on one side only fails here, on the CPU."""
+    import efl  # noqa: F401  (puts the package on sys.path)
+    from efl.privacy.paillier_cipher import PlKey
+    names = [f[0] for f in PlKey._fields_]
+    src = tmp_path / "pl_key.c"
+    src.write_text("#include <stddef.h>\n#include <stdio.h>\n#include \"efl_hip.h\"\nint main(void) {\n"
+                   "  printf(\"%zu\\n\", sizeof(efl_pl_key));\n"
+                   + "".join(f"  printf(\"%zu\\n\", offsetof(efl_pl_key, {n}));\n" for n in names)
+                   + "  return 0;\n}\n")
+    exe = tmp_path / "pl_key"
+    subprocess.check_call(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    got = [int(s) for s in subprocess.check_output([str(exe)]).split()]
+    assert got[0] == ctypes.sizeof(PlKey)
+    assert got[1:] == [getattr(PlKey, n).offset for n in names]
+
+
 def test_library_is_gfx950_code_object():
     blob = open(LIB, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob
