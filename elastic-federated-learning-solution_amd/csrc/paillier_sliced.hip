@@ -430,12 +430,13 @@ __global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_powm2
 // Instead of one square-and-multiply per term (bits(|y|) - 1 + d squarings each), the terms of
 // one sign share the squarings (Straus): from the top bit level down, square the product once,
 // then multiply in every x_ij whose exponent has that bit. Squarings drop from sum_j (bits + d) to
-// max_j (bits + d) per sign; multiplies stay popcount(|y|) per term. x_ij R (radix 2^28) is
+// max_j (bits + d) per sign; multiplies stay popcount(|y|) per term (the first is a copy). x_ij R (radix 2^28) is
 // computed once per x element (k_tomont28) instead of once per output, and read from HBM as the
 // register operand of the multiply; the two running products are the LDS operand.
 //
 // Groups walk the outputs column by column (consecutive groups: consecutive rows, the same column
-// of y), so the groups of a wave share every term's |y| and differ only through d.
+// of y), so the groups of a wave share every term's |y| and differ only through d; they also have
+// the same number of multiplies (sum of popcount(|y|)), so their event lists are about equally long.
 
 // padded radix-2^28 slice of one element in HBM: lane g's C28 limbs at [g * CP, g * CP + C28)
 template <int C28>
@@ -505,35 +506,52 @@ __global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_matmu
     const long long lvl = xr[j] + ec[(long long)j * w] - mn + (64 - __clzll((long long)ay));
     top = lvl > top ? lvl : top;
   }
-  bool started0 = false, started1 = false;   // products still 1 skip their squarings
-  for (long long b = top - 1; b >= 0; --b) {
-#pragma unroll
-    for (int sgn = 0; sgn < 2; ++sgn) {
-      if (!(sgn ? started1 : started0)) continue;
-      from_lds<C28>(t, ACC[sgn], E, g);
-      s28::mont_mul<C28, G>(t, LdsElem{ACC[sgn], E}, m28, minv28, g);
-      lds_sync();
-      to_lds<C28>(ACC[sgn], E, g, t);
-      lds_sync();
-    }
-    for (int j = 0; j < v; ++j) {
-      const long long y = yc[(long long)j * w];
-      const long long p = b - (xr[j] + ec[(long long)j * w] - mn);
-      if (y == 0 || p < 0 || p >= 64) continue;
-      const uint64_t ay = y < 0 ? 0ull - (uint64_t)y : (uint64_t)y;
-      if (!((ay >> p) & 1ull)) continue;
-      const bool neg = y < 0;
-      uint32_t* acc = neg ? ACC[1] : ACC[0];
-      load28<C28>(t, Xm + ((long long)row * v + j) * (CP * G) + g * CP);
-      if (neg ? started1 : started0) {
-        s28::mont_mul<C28, G>(t, LdsElem{acc, E}, m28, minv28, g);
-        lds_sync();
+  // Each group walks its own event list: per bit level from the top, a squaring of each started
+  // product, then one multiply per term whose exponent has that bit. Every pass of the loop below
+  // is one Montgomery product per group (its first operand from LDS for a squaring, from HBM for a
+  // multiply), so a wave runs max_group(events) products, not the union of its groups' levels.
+  bool started0 = false, started1 = false;   // products still 1 take their first term as a copy
+  long long b = top - 1;
+  int j = 0, phase = 0;                      // phase 0: square POS, 1: square NEG, 2: terms
+  for (;;) {
+    int op = -1, jj = 0;                     // op 0/1: square POS/NEG, 2/3: multiply x_j into POS/NEG
+    while (op < 0 && b >= 0) {
+      if (phase == 0) {
+        phase = 1;
+        if (started0) op = 0;
+      } else if (phase == 1) {
+        phase = 2;
+        j = 0;
+        if (started1) op = 1;
+      } else if (j >= v) {
+        --b;
+        phase = 0;
+      } else {
+        const long long y = yc[(long long)j * w];
+        const long long p = b - (xr[j] + ec[(long long)j * w] - mn);
+        if (y != 0 && p >= 0 && p < 64) {
+          const uint64_t ay = y < 0 ? 0ull - (uint64_t)y : (uint64_t)y;
+          if ((ay >> p) & 1ull) {
+            op = y < 0 ? 3 : 2;
+            jj = j;
+          }
+        }
+        ++j;
       }
-      to_lds<C28>(acc, E, g, t);
-      lds_sync();
-      if (neg) started1 = true;
-      else started0 = true;
     }
+    if (op < 0) break;
+    uint32_t* acc = (op & 1) ? ACC[1] : ACC[0];
+    if (op < 2) from_lds<C28>(t, acc, E, g);
+    else load28<C28>(t, Xm + ((long long)row * v + jj) * (CP * G) + g * CP);
+    const bool copy = op == 2 ? !started0 : op == 3 ? !started1 : false;
+    if (!copy) {
+      s28::mont_mul<C28, G>(t, LdsElem{acc, E}, m28, minv28, g);
+      lds_sync();
+    }
+    to_lds<C28>(acc, E, g, t);
+    lds_sync();
+    if (op == 2) started0 = true;
+    if (op == 3) started1 = true;
   }
   uint32_t* out[2] = {zpos + o * L, zneg + o * L};
 #pragma unroll
