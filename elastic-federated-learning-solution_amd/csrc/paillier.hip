@@ -506,6 +506,49 @@ __device__ __forceinline__ void lds_modsub(const LdsNum<L>& x, const LdsNum<L>& 
   }
 }
 
+// 33 bits of x starting at bit `pos` (pos >= 0; bits past the top limb read as 0)
+template <int L>
+__device__ __forceinline__ uint64_t lds_bits33(const LdsNum<L>& x, int pos) {
+  const int w = pos >> 5, off = pos & 31;
+  const uint64_t lo = x[w];
+  const uint64_t mid = w + 1 < L ? x[w + 1] : 0u;
+  const uint64_t hi = w + 2 < L ? x[w + 2] : 0u;
+  const uint64_t v = (lo >> off) | (mid << (32 - off)) | (off ? hi << (64 - off) : 0ull);
+  return v & ((1ull << 33) - 1);
+}
+
+// one signed limb of sum(p_i) + c, p_i = int64 products: low 32 bits out, signed carry kept
+__device__ __forceinline__ uint32_t signed_limb(int64_t p0, int64_t p1, int64_t& c) {
+  const uint64_t lo = (uint64_t)(uint32_t)p0 + (uint32_t)p1 + (uint32_t)c;
+  c = (p0 >> 32) + (p1 >> 32) + (c >> 32) + (int64_t)(lo >> 32);
+  return (uint32_t)lo;
+}
+
+__device__ __forceinline__ uint32_t signed_limb3(int64_t p0, int64_t p1, int64_t p2, int64_t& c) {
+  const uint64_t lo = (uint64_t)(uint32_t)p0 + (uint32_t)p1 + (uint32_t)p2 + (uint32_t)c;
+  c = (p0 >> 32) + (p1 >> 32) + (p2 >> 32) + (c >> 32) + (int64_t)(lo >> 32);
+  return (uint32_t)lo;
+}
+
+// x <- -x over limbs [0, n) (two's complement)
+template <int L>
+__device__ __forceinline__ void lds_neg(const LdsNum<L>& x, int n) {
+  uint32_t br = 0;
+  for (int j = 0; j < n; ++j) {
+    const uint64_t d = 0ull - x[j] - br;
+    x[j] = (uint32_t)d;
+    br = (uint32_t)(d >> 63);
+  }
+}
+
+// PaillierInvert (paillier.cc:267-273 mpz_invert): x^-1 mod n^2, Pornin's binary GCD with 31-step
+// batches ("Optimized Binary GCD for Modular Inversion", 2020, Algorithm 2). Each outer pass runs
+// 31 binary-GCD steps on 64-bit approximations of a and b (low 31 bits and top 33 bits, exact once
+// both fit 64 bits), collecting the update factors f0, g0, f1, g1 (|.| <= 2^31), then applies them
+// to the full numbers: (a, b) <- ((f0 a + g0 b) / 2^31, (f1 a + g1 b) / 2^31) with sign fixes, and
+// (u, v) <- the same combinations times 2^-31 mod M (one Montgomery-style step), keeping
+// a = u x, b = v x (mod M). About 2 len(M) / 31 passes of a few limb sweeps each, instead of one
+// sweep per bit; the 31 inner steps are branch-free, so a wave does not diverge in them.
 template <int LN>
 __global__ __launch_bounds__(kPlBlock) void k_invert(Key k, const uint32_t* __restrict__ x,
                                                      uint32_t* __restrict__ out, long long N,
@@ -516,53 +559,138 @@ __global__ __launch_bounds__(kPlBlock) void k_invert(Key k, const uint32_t* __re
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N) return;
   const uint32_t* M = k.at(k.d.off_n2);
-  const uint32_t minv = k.d.n2_minv;
-  LdsNum<LC> u{lds + threadIdx.x, S}, v{lds + LC * S + threadIdx.x, S};
-  LdsNum<LC> A{lds + 2 * LC * S + threadIdx.x, S}, C{lds + 3 * LC * S + threadIdx.x, S};
+  const uint32_t minv = k.d.n2_minv;   // -M^-1 mod 2^32
+  LdsNum<LC> A{lds + threadIdx.x, S}, B{lds + LC * S + threadIdx.x, S};
+  LdsNum<LC> U{lds + 2 * LC * S + threadIdx.x, S}, V{lds + 3 * LC * S + threadIdx.x, S};
   const uint32_t* xi = x + i * LC;
+  uint32_t any = 0;
   for (int j = 0; j < LC; ++j) {
-    u[j] = xi[j];
-    v[j] = M[j];
-    A[j] = j == 0 ? 1u : 0u;
-    C[j] = 0u;
+    A[j] = xi[j];
+    any |= xi[j];
+    B[j] = M[j];
+    U[j] = j == 0 ? 1u : 0u;
+    V[j] = 0u;
   }
-  // reduce u mod M first (inputs are ciphertexts < M; a single conditional subtract suffices)
-  bool ok = false;
-  const int max_iter = 4 * 32 * LC + 64;
-  for (int it = 0; it < max_iter; ++it) {
-    if (lds_is_zero<LC>(u)) {
-      // gcd in v; invertible iff v == 1
-      bool one = v[0] == 1u;
-      for (int j = 1; j < LC && one; ++j) one = v[j] == 0u;
-      ok = one;
-      break;
+  // total binary-GCD steps <= 2 len(M) - 1 (Pornin, Theorem 1); a few passes of slack
+  const int max_pass = (2 * 32 * LC - 1 + 30) / 31 + 4;
+  int top = LC - 1;
+  bool a_zero = any == 0;
+  for (int pass = 0; pass < max_pass && !a_zero; ++pass) {
+    while (top > 0 && (A[top] | B[top]) == 0u) --top;
+    const uint32_t th = A[top] | B[top];
+    int nb = 32 * top + 32 - __clz(th);
+    nb = nb < 64 ? 64 : nb;
+    uint64_t ab = (A[0] & 0x7FFFFFFFu) | (lds_bits33<LC>(A, nb - 33) << 31);
+    uint64_t bb = (B[0] & 0x7FFFFFFFu) | (lds_bits33<LC>(B, nb - 33) << 31);
+    int64_t f0 = 1, g0 = 0, f1 = 0, g1 = 1;
+#pragma unroll
+    for (int s = 0; s < 31; ++s) {
+      const bool odd = ab & 1ull;
+      const bool sw = odd && ab < bb;
+      const uint64_t ta = sw ? bb : ab, tb = sw ? ab : bb;
+      const int64_t tf0 = sw ? f1 : f0, tg0 = sw ? g1 : g0, tf1 = sw ? f0 : f1, tg1 = sw ? g0 : g1;
+      ab = (odd ? ta - tb : ta) >> 1;
+      bb = tb;
+      f0 = odd ? tf0 - tf1 : tf0;
+      g0 = odd ? tg0 - tg1 : tg0;
+      f1 = tf1 << 1;
+      g1 = tg1 << 1;
     }
-    uint32_t w = u[0];
-    while (!(w & 1u)) {
-      const int kk = w ? __builtin_ctz(w) : 31;
-      const int sh = kk > 31 ? 31 : kk;
-      lds_shr<LC>(u, sh);
-      lds_half_k<LC>(A, sh, M, minv);
-      w = u[0];
+    // (a, b) <- ((f0 a + g0 b) >> 31, (f1 a + g1 b) >> 31) over limbs [0, top]; values do not grow
+    {
+      int64_t ca = 0, cb = 0;
+      uint32_t pa = 0, pb = 0, nz = 0;
+      for (int j = 0; j <= top; ++j) {
+        const int64_t aj = A[j], bj = B[j];
+        const uint32_t da = signed_limb(aj * f0, bj * g0, ca);
+        const uint32_t db = signed_limb(aj * f1, bj * g1, cb);
+        if (j) {
+          A[j - 1] = (pa >> 31) | (da << 1);
+          B[j - 1] = (pb >> 31) | (db << 1);
+          nz |= A[j - 1];
+        }
+        pa = da;
+        pb = db;
+      }
+      A[top] = (pa >> 31) | ((uint32_t)ca << 1);
+      B[top] = (pb >> 31) | ((uint32_t)cb << 1);
+      nz |= A[top];
+      if (ca < 0) {
+        lds_neg<LC>(A, top + 1);
+        f0 = -f0;
+        g0 = -g0;
+      }
+      if (cb < 0) {
+        lds_neg<LC>(B, top + 1);
+        f1 = -f1;
+        g1 = -g1;
+      }
+      a_zero = nz == 0u;
     }
-    w = v[0];
-    while (!(w & 1u)) {
-      const int kk = w ? __builtin_ctz(w) : 31;
-      const int sh = kk > 31 ? 31 : kk;
-      lds_shr<LC>(v, sh);
-      lds_half_k<LC>(C, sh, M, minv);
-      w = v[0];
-    }
-    if (lds_geq<LC>(u, v)) {
-      lds_sub<LC>(u, v);
-      lds_modsub<LC>(A, C, M);
-    } else {
-      lds_sub<LC>(v, u);
-      lds_modsub<LC>(C, A, M);
+    // (u, v) <- ((f0 u + g0 v) 2^-31, (f1 u + g1 v) 2^-31) mod M: add t M with the low 31 bits of
+    // the sum zeroed, shift, then bring the result (|r| < 3M) into [0, M)
+    {
+      const uint32_t s0u = U[0] * (uint32_t)f0 + V[0] * (uint32_t)g0;
+      const uint32_t s0v = U[0] * (uint32_t)f1 + V[0] * (uint32_t)g1;
+      const int64_t tu = (int64_t)((s0u * minv) & 0x7FFFFFFFu), tv = (int64_t)((s0v * minv) & 0x7FFFFFFFu);
+      int64_t cu = 0, cv = 0;
+      uint32_t pu = 0, pv = 0;
+      for (int j = 0; j < LC; ++j) {
+        const int64_t uj = U[j], vj = V[j], mj = M[j];
+        const uint32_t ru = signed_limb3(uj * f0, vj * g0, tu * mj, cu);
+        const uint32_t rv = signed_limb3(uj * f1, vj * g1, tv * mj, cv);
+        if (j) {
+          U[j - 1] = (pu >> 31) | (ru << 1);
+          V[j - 1] = (pv >> 31) | (rv << 1);
+        }
+        pu = ru;
+        pv = rv;
+      }
+      U[LC - 1] = (pu >> 31) | ((uint32_t)cu << 1);
+      V[LC - 1] = (pv >> 31) | ((uint32_t)cv << 1);
+      int64_t eu = cu >> 31, ev = cv >> 31;   // limb LC of the shifted results (small, signed)
+#pragma unroll
+      for (int which = 0; which < 2; ++which) {
+        const LdsNum<LC>& R = which ? V : U;
+        int64_t& ext = which ? ev : eu;
+        while (ext < 0) {   // R += M
+          uint32_t c = 0;
+          for (int j = 0; j < LC; ++j) {
+            const uint64_t t = (uint64_t)R[j] + M[j] + c;
+            R[j] = (uint32_t)t;
+            c = (uint32_t)(t >> 32);
+          }
+          ext += c;
+        }
+        for (;;) {          // R >= M (or ext > 0): R -= M
+          bool ge = ext > 0;
+          if (!ge) {
+            ge = true;
+            for (int j = LC - 1; j >= 0; --j) {
+              const uint32_t r = R[j], m = M[j];
+              if (r != m) {
+                ge = r > m;
+                break;
+              }
+            }
+          }
+          if (!ge) break;
+          uint32_t br = 0;
+          for (int j = 0; j < LC; ++j) {
+            const uint64_t d = (uint64_t)R[j] - M[j] - br;
+            R[j] = (uint32_t)d;
+            br = (uint32_t)(d >> 63);
+          }
+          ext -= br;
+        }
+      }
     }
   }
+  // gcd in b: invertible iff a reached 0 with b == 1
+  bool ok = a_zero && B[0] == 1u;
+  for (int j = 1; j < LC && ok; ++j) ok = B[j] == 0u;
   uint32_t* o = out + i * LC;
-  for (int j = 0; j < LC; ++j) o[j] = ok ? C[j] : 0u;
+  for (int j = 0; j < LC; ++j) o[j] = ok ? V[j] : 0u;
   if (!ok) atomicMin(bad, (unsigned long long)i);
 }
 

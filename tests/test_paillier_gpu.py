@@ -216,6 +216,31 @@ def test_invert_and_negative_scalars(efl, c):
         _invert_and_negative_scalars(efl, k, kp)
 
 
+@pytest.mark.parametrize("k", ALL, ids=ids)
+def test_invert_random_and_edges(efl, k):
+    """Batched binary GCD (k_invert) against exact Python inverses mod n^2 for every key size: 512
+    random units, 1, n^2 - 1, 2, small and top-heavy values; non-units (a multiple of p, 0) give
+    the 'no inverse' error."""
+    kp = keypair(efl, k, private=False)
+    n = int(k["n"], 16)
+    n2 = n * n
+    rng = random.Random(k["n_bytes"])
+    xs = [rng.randrange(1, n2) for _ in range(512)]
+    xs += [1, n2 - 1, 2, 3, (1 << 64) + 1, n2 - 2, n2 >> 1, (n2 >> 1) + 1]
+    want = []
+    for x in xs:
+        try:
+            want.append(pow(x, -1, n2))
+        except ValueError:
+            want.append(None)
+    units = [x for x, w in zip(xs, want) if w is not None]
+    got = kp.invert(efl.HexTensor.from_ints(units)).to_hex().to_ints()
+    assert got == [w for w in want if w is not None]
+    p = int(k["p"], 16)
+    with pytest.raises(efl.errors.InvalidArgumentError, match="no inverse"):
+        kp.invert(efl.HexTensor.from_ints([units[0], p * 12345, 0]))
+
+
 def _invert_and_negative_scalars(efl, k, kp):
     okp = P.Keypair(int(k["n"], 16), int(k["hs"], 16), k["a_bits"] // 8, 1, int(k["p"], 16), int(k["q"], 16))
     cs = [int(v["c"], 16) for v in k["vectors"][:12]]
