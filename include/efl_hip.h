@@ -9,8 +9,9 @@
  * types. The Python drop-in (package `efl`, ctypes) and INTEGRATION.md show the binding.
  *
  * Conventions
- *  - Every payload pointer is DEVICE memory owned by the caller; the library never allocates
- *    payload memory and never synchronises: work is enqueued on `stream` (NULL = default stream).
+ *  - Every payload pointer is DEVICE memory owned by the caller; the library never synchronises:
+ *    work is enqueued on `stream` (NULL = default stream). It allocates nothing except the
+ *    stream-ordered scratch of efl_pl_matmul (see there).
  *  - Return value: 0 on success, otherwise the NEGATED TensorFlow error code
  *    (tensorflow/core/lib/core/error_codes.proto; the reference reports errors as TF Status):
  *      -3 INVALID_ARGUMENT, -8 RESOURCE_EXHAUSTED, -9 FAILED_PRECONDITION, -10 ABORTED,
@@ -220,7 +221,9 @@ int efl_pl_invert(const void* key_block, const efl_pl_key* key, const uint32_t* 
 /* PaillierMatmul (paillier.cc:915-1053) core: x_mantissa [u][v] ciphertexts, x_exponent [u][v],
  * y_mantissa / y_exponent [v][w] int64. For each output z_exponent = min_j(xe + ye) and the terms
  * (x^|y|)^(2^(xe + ye - min)) are multiplied into z_pos (y > 0) or z_neg (y < 0); the caller
- * finishes z = z_pos * z_neg^-1 (efl_pl_invert + efl_pl_add). */
+ * finishes z = z_pos * z_neg^-1 (efl_pl_invert + efl_pl_add). With the radix-2^28 family the
+ * kernel first writes x R mod n^2 for every x into u*v*L28*4 bytes of scratch taken and released
+ * on `stream` (hipMallocAsync / hipFreeAsync); a failed allocation returns the HIP error. */
 int efl_pl_matmul(const void* key_block, const efl_pl_key* key, const uint32_t* x_mantissa,
                   const int64_t* x_exponent, const int64_t* y_mantissa, const int64_t* y_exponent,
                   uint32_t* z_pos, uint32_t* z_neg, int64_t* z_exponent, int u, int v, int w,
