@@ -856,9 +856,22 @@ inline bool key_ok(const efl_pl_key* d, bool need_private, int ln_max) {
 
 // kernel family per key size: 0 = one lane per element (paillier.hip), C = sliced over 2ln/C (n^2
 // ops) or ln/C (decryption) lanes of C limbs (paillier_sliced.hip). [ln 16/32/64/128][n^2 ops, decrypt]
-int g_slicing[4][2] = {{16, 8}, {16, 32}, {16, 32}, {8, 32}};   // measured: profiles/r01/bench_pl*.jsonl
+constexpr int kDefaultSlicing[4][2] = {{16, 8}, {16, 32}, {16, 32}, {8, 32}};   // measured: profiles/r01/bench_pl*.jsonl
+int g_slicing[4][2] = {{16, 8}, {16, 32}, {16, 32}, {8, 32}};
 inline int ln_index(int ln) { return ln == 16 ? 0 : ln == 32 ? 1 : ln == 64 ? 2 : 3; }
 inline int slicing(int ln, int dec) { return g_slicing[ln_index(ln)][dec]; }
+bool g_slicing_set[4][2] = {};   // set explicitly through efl_pl_tune: used as given for every size
+
+// Decryption family for n elements: the default (measured at >= 100k elements) unless the launch
+// would leave SIMDs without a wave; then more lanes per element (profiles/r01/sweep_small_n.jsonl:
+// 32k decrypts at 1024-bit, 2.57 M/s with 32 limbs per lane, 3.29 M/s with 16)
+inline int decrypt_family(int ln, long long n) {
+  int C = slicing(ln, 1);
+  if (!C || g_slicing_set[ln_index(ln)][1]) return C;
+  constexpr long long kOneWavePerSimd = 256ll * 4 * 64;
+  while (C > 8 && n * (ln / C) < kOneWavePerSimd && pl::sliced_available(ln, C / 2)) C /= 2;
+  return C;
+}
 
 inline unsigned grid_of(long long N) { return (unsigned)((N + kPlBlock - 1) / kPlBlock); }
 
@@ -981,7 +994,7 @@ EFL_API int efl_pl_decrypt(const void* key_block, const efl_pl_key* key, const u
   Key k{(const uint32_t*)key_block, *key};
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;
-  const int C = slicing(key->ln, 1);
+  const int C = decrypt_family(key->ln, n);
   if (C) return hip_status(pl::sl_decrypt(k, C, ciphertext, magnitude, (signed char*)negative, n, s), "efl_pl_decrypt");
   switch (key->ln) {
     case 16: e = run_decrypt<16>(k, ciphertext, magnitude, (signed char*)negative, n, s); break;
@@ -1056,6 +1069,12 @@ EFL_API int efl_pl_matmul(const void* key_block, const efl_pl_key* key, const ui
 EFL_API int efl_pl_tune(int ln, int decrypt, int limbs_per_lane) {
   if (ln != 16 && ln != 32 && ln != 64 && ln != 128) { set_error("unsupported limb count %d", ln); return EFL_E_INVALID_ARGUMENT; }
   const int dec = decrypt ? 1 : 0;
+  if (limbs_per_lane == -2) {                       // back to the measured default, sized per launch
+    const int prev = slicing(ln, dec);
+    g_slicing[ln_index(ln)][dec] = kDefaultSlicing[ln_index(ln)][dec];
+    g_slicing_set[ln_index(ln)][dec] = false;
+    return prev;
+  }
   if (limbs_per_lane < 0) return slicing(ln, dec);   // query
   if (limbs_per_lane == 0) {
     if (!dec && ln > 64) { set_error("no one-lane kernels for n^2 of %d bits", 64 * ln); return EFL_E_INVALID_ARGUMENT; }
@@ -1065,6 +1084,7 @@ EFL_API int efl_pl_tune(int ln, int decrypt, int limbs_per_lane) {
   }
   const int prev = slicing(ln, dec);
   g_slicing[ln_index(ln)][dec] = limbs_per_lane;
+  g_slicing_set[ln_index(ln)][dec] = true;
   return prev;
 }
 

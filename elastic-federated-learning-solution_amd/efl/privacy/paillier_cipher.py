@@ -83,6 +83,14 @@ def set_kernel_slicing(ln: int, decrypt: bool, limbs_per_lane: int) -> int:
     return rc
 
 
+def reset_kernel_slicing(ln: int, decrypt: bool) -> int:
+    """Back to the measured default family (decryption then also sizes it per launch)."""
+    rc = _lib.efl_pl_tune(ln, int(bool(decrypt)), -2)
+    if rc < 0:
+        _efl_lib.check(rc)
+    return rc
+
+
 # kernel families compiled per key size (ln): n^2 ops, decryption
 SLICINGS = {16: ([0, 8, 16, 32], [0, 8]), 32: ([0, 8, 16, 32], [0, 8, 16, 32]), 64: ([0, 8, 16, 32], [0, 8, 16, 32]),
             128: ([8, 16, 32], [0, 8, 16, 32])}

@@ -232,8 +232,10 @@ int efl_pl_matmul(const void* key_block, const efl_pl_key* key, const uint32_t* 
 /* Kernel family for keys of ln limbs (16/32/64/128): decrypt = 0 selects the n^2 ops (encrypt,
  * fbpowm, add, powm, matmul), 1 decryption. limbs_per_lane 0 = one lane per element (n^2 ops:
  * ln <= 64 only), 16 or 32 = one number spread over L/limbs_per_lane lanes (L = 2 ln, or ln for
- * decryption); -1 queries. Returns the previous choice, or a negative error code. Results are
- * identical across families; only speed differs. */
+ * decryption); -1 queries; -2 restores the default. Returns the previous choice, or a negative
+ * error code. Results are identical across families; only speed differs. With the default
+ * (never set, or restored by -2) a decryption of too few elements to give every SIMD a wave takes
+ * more lanes per element; a family set explicitly is used for every size. */
 int efl_pl_tune(int ln, int decrypt, int limbs_per_lane);
 
 /* mpz_get_str(..., 16) of n numbers ([n][limbs_per_elem], optional sign bytes): first the text

@@ -217,6 +217,24 @@ def test_invert_and_negative_scalars(efl, c):
 
 
 @pytest.mark.parametrize("k", ALL, ids=ids)
+@pytest.mark.parametrize("n", [1, 100, 5000, 40000])
+def test_decrypt_default_family_sized_per_launch(efl, k, n):
+    """With the default family, small decryptions take more lanes per element (decrypt_family);
+    results stay exact at every size."""
+    from efl.privacy import paillier_cipher as pc
+    ln = k["n_bytes"] // 4
+    prev = pc.reset_kernel_slicing(ln, True)
+    try:
+        kp = keypair(efl, k)
+        gen = torch.Generator(device="cuda").manual_seed(n)
+        m = torch.randint(-2**62, 2**62, (n,), dtype=torch.int64, device="cuda", generator=gen)
+        got = kp.decrypt(kp.encrypt(m), dtype=torch.int64)
+        assert torch.equal(got, m)
+    finally:
+        pc.set_kernel_slicing(ln, True, prev)
+
+
+@pytest.mark.parametrize("k", ALL, ids=ids)
 def test_invert_random_and_edges(efl, k):
     """Batched binary GCD (k_invert) against exact Python inverses mod n^2 for every key size: 512
     random units, 1, n^2 - 1, 2, small and top-heavy values; non-units (a multiple of p, 0) give
