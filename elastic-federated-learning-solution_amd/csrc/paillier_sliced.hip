@@ -477,13 +477,15 @@ template <int C, int G>
 __global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_matmul28(
     Key k, const uint32_t* __restrict__ Xm, const long long* __restrict__ xe, const long long* __restrict__ ym,
     const long long* __restrict__ ye, uint32_t* __restrict__ zpos, uint32_t* __restrict__ zneg,
-    long long* __restrict__ ze, int u, int v, int w) {
+    long long* __restrict__ ze, int u, int v, int w, int S, uint32_t* __restrict__ P) {
   constexpr int L = C * G, E = kSlBlock / G;
   constexpr int C28 = s28::limbs_per_lane(L, G), L28 = C28 * G, CP = pad4<C28>();
   extern __shared__ uint32_t lds[];
   SL_ELEMENT(E, G)
-  if (i >= (long long)u * w) return;
-  const int row = (int)(i % u), kk = (int)(i / u);
+  const long long UW = (long long)u * w;
+  if (i >= UW * S) return;
+  const int sp = (int)(i / UW);                      // split of the terms this group takes
+  const int row = (int)(i % UW % u), kk = (int)(i % UW / u);
   const long long o = (long long)row * w + kk;
   uint32_t* ACC[2] = {lds + e, lds + L28 * E + e};   // running products: y > 0, y < 0
   uint32_t m28[C28], t[C28];
@@ -497,9 +499,10 @@ __global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_matmu
     const long long ex = xr[j] + ec[(long long)j * w];
     mn = ex < mn ? ex : mn;
   }
-  // top bit level of any term's exponent |y| 2^d
+  // this split's terms [j0, j1); top bit level of any of their exponents |y| 2^d
+  const int j0 = (int)((long long)v * sp / S), j1 = (int)((long long)v * (sp + 1) / S);
   long long top = 0;
-  for (int j = 0; j < v; ++j) {
+  for (int j = j0; j < j1; ++j) {
     const long long y = yc[(long long)j * w];
     if (y == 0) continue;
     const uint64_t ay = y < 0 ? 0ull - (uint64_t)y : (uint64_t)y;
@@ -521,9 +524,9 @@ __global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_matmu
         if (started0) op = 0;
       } else if (phase == 1) {
         phase = 2;
-        j = 0;
+        j = j0;
         if (started1) op = 1;
-      } else if (j >= v) {
+      } else if (j >= j1) {
         --b;
         phase = 0;
       } else {
@@ -553,6 +556,21 @@ __global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_matmu
     if (op == 2) started0 = true;
     if (op == 3) started1 = true;
   }
+  if (S > 1) {
+    // partial products (radix-2^28 Montgomery form, < 2m) for k_matcomb28; 1 = R for an unused sign
+#pragma unroll
+    for (int sgn = 0; sgn < 2; ++sgn) {
+      if (sgn ? started1 : started0) from_lds<C28>(t, ACC[sgn], E, g);
+      else slice_uniform<C28>(t, k.at(k.d.off_n2_one28), g);
+      uint32_t* q = P + (((long long)sp * UW + o) * 2 + sgn) * (CP * G) + g * CP;
+#pragma unroll
+      for (int jj = 0; jj < CP; jj += 4)
+        *reinterpret_cast<uint4*>(q + jj) = make_uint4(t[jj], jj + 1 < C28 ? t[jj + 1] : 0u,
+                                                       jj + 2 < C28 ? t[jj + 2] : 0u, jj + 3 < C28 ? t[jj + 3] : 0u);
+    }
+    if (sp == 0 && g == 0) ze[o] = mn;
+    return;
+  }
   uint32_t* out[2] = {zpos + o * L, zneg + o * L};
 #pragma unroll
   for (int sgn = 0; sgn < 2; ++sgn) {
@@ -569,6 +587,36 @@ __global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_matmu
     lds_sync();
   }
   if (g == 0) ze[o] = mn;
+}
+
+// z_pos / z_neg from the S partial products of each output (k_matmul28 with S > 1)
+template <int C, int G>
+__global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_matcomb28(
+    Key k, const uint32_t* __restrict__ P, int S, long long UW, uint32_t* __restrict__ zpos,
+    uint32_t* __restrict__ zneg) {
+  constexpr int L = C * G, E = kSlBlock / G;
+  constexpr int C28 = s28::limbs_per_lane(L, G), CP = pad4<C28>();
+  extern __shared__ uint32_t lds[];
+  SL_ELEMENT(E, G)
+  if (i >= UW * 2) return;
+  const long long o = i >> 1;
+  const int sgn = (int)(i & 1);
+  uint32_t* B = lds + e;
+  uint32_t m28[C28], t[C28], r[C28];
+  slice_uniform<C28>(m28, k.at(k.d.off_n2_28), g);
+  const uint32_t minv28 = k.d.n2_minv28;
+  const long long stride = UW * 2 * (CP * G);
+  const uint32_t* q = P + (o * 2 + sgn) * (CP * G) + g * CP;
+  load28<C28>(t, q);
+  for (int sp = 1; sp < S; ++sp) {
+    load28<C28>(r, q + sp * stride);
+    lds_sync();
+    to_lds<C28>(B, E, g, r);
+    lds_sync();
+    s28::mont_mul<C28, G>(t, LdsElem{B, E}, m28, minv28, g);
+  }
+  lds_sync();
+  store_from_mont28<C, G>((sgn ? zneg : zpos) + o * L, t, m28, minv28, B, E, g);
 }
 
 // PaillierMatmul core, one group per output (see paillier.hip k_matmul)
@@ -849,15 +897,27 @@ template <int C, int G>
 hipError_t run_matmul28(const Key& k, const uint32_t* X, const long long* xe, const long long* ym, const long long* ye,
                         uint32_t* zpos, uint32_t* zneg, long long* ze, int u, int v, int w, hipStream_t s) {
   constexpr int C28 = s28::limbs_per_lane(C * G, G), L28 = C28 * G, E = kSlBlock / G;
-  const long long nx = (long long)u * v;
-  uint32_t* Xm = nullptr;   // x R mod n^2 in padded radix-2^28 slices, stream-ordered scratch
-  hipError_t err = hipMallocAsync(reinterpret_cast<void**>(&Xm), (size_t)nx * pad4<C28>() * G * 4, s);
+  const long long nx = (long long)u * v, UW = (long long)u * w;
+  // terms split S ways over separate groups when one group per output would leave SIMDs with
+  // fewer than 4 waves (the occupancy the kernel's register bound allows); partials combined after
+  constexpr long long kFourWavesPerSimd = 256ll * 4 * 64 * 4;
+  int S = 1;
+  while (2 * S <= 8 && 2 * S <= v && UW * G * S < kFourWavesPerSimd) S *= 2;
+  const size_t slot = (size_t)pad4<C28>() * G;
+  uint32_t* Xm = nullptr;   // x R mod n^2 in padded radix-2^28 slices, then the partials: stream-ordered scratch
+  hipError_t err = hipMallocAsync(reinterpret_cast<void**>(&Xm), ((size_t)nx + (S > 1 ? (size_t)S * UW * 2 : 0)) * slot * 4, s);
   if (err != hipSuccess) return err;
+  uint32_t* P = S > 1 ? Xm + (size_t)nx * slot : nullptr;
   hipLaunchKernelGGL((k_tomont28<C, G>), dim3(grid_of(nx, G)), dim3(kSlBlock), (size_t)L28 * E * 4, s, k, X, Xm, nx);
   err = hipGetLastError();
   if (err == hipSuccess) {
-    hipLaunchKernelGGL((k_matmul28<C, G>), dim3(grid_of((long long)u * w, G)), dim3(kSlBlock),
-                       (size_t)2 * L28 * E * 4, s, k, Xm, xe, ym, ye, zpos, zneg, ze, u, v, w);
+    hipLaunchKernelGGL((k_matmul28<C, G>), dim3(grid_of(UW * S, G)), dim3(kSlBlock), (size_t)2 * L28 * E * 4, s, k,
+                       Xm, xe, ym, ye, zpos, zneg, ze, u, v, w, S, P);
+    err = hipGetLastError();
+  }
+  if (err == hipSuccess && S > 1) {
+    hipLaunchKernelGGL((k_matcomb28<C, G>), dim3(grid_of(UW * 2, G)), dim3(kSlBlock), (size_t)L28 * E * 4, s, k, P,
+                       S, UW, zpos, zneg);
     err = hipGetLastError();
   }
   const hipError_t ferr = hipFreeAsync(Xm, s);

@@ -301,6 +301,33 @@ def _matmul_vs_oracle(efl):
     assert dec == want
 
 
+def test_matmul_many_outputs_plaintext(efl):
+    """Enough outputs that every one gets its own group (no term split, k_matmul28 with S = 1; the
+    small oracle cases above take the split + combine path): exact plaintexts of sampled outputs,
+    both signs, zeros and exponent spreads."""
+    k = ENC_KEYS[0]
+    kp = keypair(efl, k)
+    rng = np.random.default_rng(11)
+    u, v, w = 512, 3, 256
+    xm = rng.integers(-2**30, 2**30, (u, v))
+    xe = rng.integers(-40, -5, (u, v))
+    ym = rng.integers(-2**11, 2**11, (v, w))
+    ym[1, ::7] = 0
+    ye = rng.integers(-30, -3, (v, w))
+    ct = kp.encrypt(torch.from_numpy(xm))
+    zm, ze = kp.matmul(ct.tensor, torch.from_numpy(xe), torch.from_numpy(ym), torch.from_numpy(ye))
+    ze = ze.cpu().numpy()
+    ex = xe[:, :, None] + ye[None, :, :]
+    assert np.array_equal(ze, ex.min(axis=1))
+    pick = rng.choice(u * w, 200, replace=False)
+    from efl.privacy import paillier_cipher as pc
+    sub = pc.CipherTensor(zm.limbs[torch.from_numpy(pick).to(zm.limbs.device)], (len(pick),), kp.key)
+    dec = kp.decrypt(sub, dtype="string").to_ints()
+    for o, got in zip(pick.tolist(), dec):
+        i, q = divmod(o, w)
+        assert got == sum(int(xm[i, j]) * int(ym[j, q]) << int(ex[i, j, q] - ze[i, q]) for j in range(v)), o
+
+
 def test_fixed_point_matmul_and_mul_like_reference_test(efl):
     """paillier_test.py:49-79 (mul_scalar, matmul) with a 512-bit key; exact plaintext check."""
     kp = efl.paillier.Keypair()
