@@ -269,15 +269,25 @@ def stage_p_matmul(args, efl, pc, kp, lib, sh, stream, dev):
         hit = (ay >> q) & 1
         pop += hit
         bits = np.where(hit == 1, q + 1, bits)
-    products = u * v
-    for mask in (nz & (ym_h > 0), nz & (ym_h < 0)):
-        top = np.where(mask[None, :, :], d + bits[None, :, :], 0).max(axis=1)    # [u, w]
-        started = mask.any(axis=0)[None, :].repeat(u, axis=0)
-        products += int(np.maximum(top - 1, 0)[started].sum()) + u * int(pop[mask].sum()) - int(started.sum())
-        products += int(started.sum())
-    per_term = u * int((bits + pop)[nz].sum()) + int((d * nz[None, :, :]).sum()) + 2 * u * w
     L = k.lc
     fam = pc.kernel_slicing(k.ln, False)
+    # the term split of run_matmul28 (csrc/paillier_sliced.hip): each split squares on its own
+    S, G = 1, (L // fam if fam else 1)
+    while 2 * S <= 8 and 2 * S <= v and u * w * G * S < 256 * 4 * 64 * 8:
+        S *= 2
+    products = u * v + (2 * S * u * w if S > 1 else 0)      # x R; combining the partials + conversion out
+    for sp in range(S):
+        j0, j1 = v * sp // S, v * (sp + 1) // S
+        for sgn in (1, -1):
+            mask = np.zeros_like(nz)
+            mask[j0:j1] = nz[j0:j1] & (np.sign(ym_h[j0:j1]) == sgn)
+            top = np.where(mask[None, :, :], d + bits[None, :, :], 0).max(axis=1)    # [u, w]
+            started = mask.any(axis=0)[None, :].repeat(u, axis=0)
+            # squarings below the top level, multiplies less the first (a copy), one conversion out
+            products += int(np.maximum(top - 1, 0)[started].sum()) + u * int(pop[mask].sum()) - int(started.sum())
+            if S == 1:
+                products += int(started.sum())
+    per_term = u * int((bits + pop)[nz].sum()) + int((d * nz[None, :, :]).sum()) + 2 * u * w
     L_issued = k.desc.n2_28_len if (fam and k.desc.off_table28 >= 0) else L
     macs, issued = 2 * L * L * products, 2 * L_issued * L_issued * products
     # the whole op as the layer calls it (kernel + z_neg^-1 + z_pos * z_neg^-1), then a plaintext
@@ -300,7 +310,7 @@ def stage_p_matmul(args, efl, pc, kp, lib, sh, stream, dev):
             raise SystemExit(f"bench: PaillierMatmul output {o} is wrong")
     res = {"shape": [u, v, w], "outputs_per_s": round(u * w / t, 1), "ms": round(t * 1e3, 3),
            "op_ms": round(t_op * 1e3, 3), "op_outputs_per_s": round(u * w / t_op, 1),
-           "montgomery_products_per_output": round(products / (u * w), 1),
+           "term_splits": S, "montgomery_products_per_output": round(products / (u * w), 1),
            "per_term_products_per_output": round(per_term / (u * w), 1),
            "roofline": {"bound": "valu", "achieved": round(macs / t / 1e12, 3),
                         "peak": round(MAD_U64_U32_PEAK / 1e12, 3), "unit": "TMAC/s",

@@ -898,11 +898,12 @@ hipError_t run_matmul28(const Key& k, const uint32_t* X, const long long* xe, co
                         uint32_t* zpos, uint32_t* zneg, long long* ze, int u, int v, int w, hipStream_t s) {
   constexpr int C28 = s28::limbs_per_lane(C * G, G), L28 = C28 * G, E = kSlBlock / G;
   const long long nx = (long long)u * v, UW = (long long)u * w;
-  // terms split S ways over separate groups when one group per output would leave SIMDs with
-  // fewer than 4 waves (the occupancy the kernel's register bound allows); partials combined after
-  constexpr long long kFourWavesPerSimd = 256ll * 4 * 64 * 4;
+  // terms split S ways over separate groups when one group per output would give fewer than two
+  // rounds of 4 waves per SIMD (the occupancy the register bound allows; a second round evens out
+  // the groups' unequal event counts); partials combined after. bench.py mirrors this choice.
+  constexpr long long kTwoRoundsOfFourWaves = 256ll * 4 * 64 * 8;
   int S = 1;
-  while (2 * S <= 8 && 2 * S <= v && UW * G * S < kFourWavesPerSimd) S *= 2;
+  while (2 * S <= 8 && 2 * S <= v && UW * G * S < kTwoRoundsOfFourWaves) S *= 2;
   const size_t slot = (size_t)pad4<C28>() * G;
   uint32_t* Xm = nullptr;   // x R mod n^2 in padded radix-2^28 slices, then the partials: stream-ordered scratch
   hipError_t err = hipMallocAsync(reinterpret_cast<void**>(&Xm), ((size_t)nx + (S > 1 ? (size_t)S * UW * 2 : 0)) * slot * 4, s);
