@@ -1,0 +1,261 @@
+// Secret-sharing masks: the additive float noise EFLS applies to a tensor
+// before the communicator sends one share of it cross-silo.
+//
+// Reference: efls-train/python/efl/privacy/secret_sharing.py
+//   generate_suitable_noise(t) = tf.random.uniform(shape(t)) * t                        (:26-27)
+//   share():       send a = noise(x), keep x - a                                        (:158-168)
+//   Dense weights: send w - noise(w)/d, keep w + noise(w)/d                             (:137-143)
+//   _matmul mode A (column pairs of e = noise(a)): send [a + e | e_even + e_odd],
+//                  keep a - e and e_odd - e_even                                        (:30-41)
+//   _matmul mode B (row pairs of f = noise(b)):    send [b/2 - f ; f_even - f_odd],
+//                  keep b/2 + f and f_odd + f_even                                      (:42-53)
+// TF draws the uniform from an unseeded Philox4x32-10 stream and converts each 32-bit word with
+// Uint32ToFloat (23 mantissa bits under exponent 127, minus 1.0). The build uses the same
+// generator and conversion, keyed by an explicit 64-bit seed with element i taking word i % 4 of
+// Philox block ctr0 + i / 4, so every output is reproducible and checkable bit for bit
+// (oracle/mask.py); the reference itself is only pinned statistically.
+//
+// Every kernel is one streaming pass: read x once, write each output once. One lane owns four
+// consecutive elements (one Philox block, dwordx4 loads and stores). HBM-bound, no LDS, no MFMA.
+#include "common.h"
+#include "pl_common.h"
+
+// Every product and sum rounds on its own, as TF's separate ops (and numpy in the oracle) do:
+// hipcc contracts a*b+c into one FMA by default, which changes the last bit.
+#pragma clang fp contract(off)
+
+namespace efl {
+namespace {
+
+using pl::philox;
+
+__device__ __forceinline__ float u01(uint32_t w) {
+  return __uint_as_float(0x3f800000u | (w & 0x7fffffu)) - 1.0f;
+}
+
+__device__ __forceinline__ void draw4(uint64_t seed, uint64_t blk, float (&u)[4]) {
+  uint32_t c[4] = {(uint32_t)blk, (uint32_t)(blk >> 32), 0u, 0u};
+  philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+#pragma unroll
+  for (int j = 0; j < 4; ++j) u[j] = u01(c[j]);
+}
+
+// noise n = U * x (then / d when d != 1, as `noise / noise_divisor` in the reference)
+__device__ __forceinline__ float noise(float u, float x, float d, bool div) {
+  const float n = u * x;
+  return div ? n / d : n;
+}
+
+// op 0: o0 = n            (generate_suitable_noise)
+// op 1: o0 = n, o1 = x-n  (share: the sent share and the kept one)
+// op 2: o0 = x-n, o1 = x+n (Dense weight noise: sent and kept)
+template <int OP>
+__global__ __launch_bounds__(kBlock) void k_noise(const float* __restrict__ x, float* __restrict__ o0,
+                                                  float* __restrict__ o1, long long n, uint64_t seed,
+                                                  uint64_t ctr0, float d, int div) {
+  const long long g = (long long)blockIdx.x * kBlock + threadIdx.x;
+  const long long i0 = g * 4;
+  if (i0 >= n) return;
+  float u[4];
+  draw4(seed, ctr0 + (uint64_t)g, u);
+  if (i0 + 4 <= n) {
+    const f4 v = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + g);
+    f4 a, b;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float nz = noise(u[j], v[j], d, div);
+      if (OP == 0) a[j] = nz;
+      if (OP == 1) { a[j] = nz; b[j] = v[j] - nz; }
+      if (OP == 2) { a[j] = v[j] - nz; b[j] = v[j] + nz; }
+    }
+    reinterpret_cast<f4*>(o0)[g] = a;
+    if (OP != 0) reinterpret_cast<f4*>(o1)[g] = b;
+  } else {
+    for (int j = 0; j < 4 && i0 + j < n; ++j) {
+      const float xv = x[i0 + j];
+      const float nz = noise(u[j], xv, d, div);
+      if (OP == 0) o0[i0 + j] = nz;
+      if (OP == 1) { o0[i0 + j] = nz; o1[i0 + j] = xv - nz; }
+      if (OP == 2) { o0[i0 + j] = xv - nz; o1[i0 + j] = xv + nz; }
+    }
+  }
+}
+
+// Mode A, a [R, C] with C % 8 == 0 (every row of send, width 3C/2, then starts 16-byte aligned):
+// lane g owns a[r, 4q .. 4q+3] (element index 4g).
+// send [R, 3C/2] = [a + e | e_even + e_odd], keep0 [R, C] = a - e, keep1 [R, C/2] = e_odd - e_even.
+__global__ __launch_bounds__(kBlock) void k_mask_cols4(const float* __restrict__ a, float* __restrict__ send,
+                                                       float* __restrict__ keep0, float* __restrict__ keep1,
+                                                       long long R, long long C, uint64_t seed, uint64_t ctr0) {
+  const long long g = (long long)blockIdx.x * kBlock + threadIdx.x;
+  const long long q4 = C / 4;
+  if (g >= R * q4) return;
+  const long long r = g / q4, q = g - r * q4;
+  float u[4];
+  draw4(seed, ctr0 + (uint64_t)g, u);
+  const f4 v = __builtin_nontemporal_load(reinterpret_cast<const f4*>(a) + g);
+  f4 s, k;
+  float e[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    e[j] = u[j] * v[j];
+    s[j] = v[j] + e[j];
+    k[j] = v[j] - e[j];
+  }
+  const long long W = C + C / 2;
+  *reinterpret_cast<f4*>(send + r * W + 4 * q) = s;
+  reinterpret_cast<f4*>(keep0)[g] = k;
+  f2 p, m;
+  p[0] = e[0] + e[1];
+  p[1] = e[2] + e[3];
+  m[0] = e[1] - e[0];
+  m[1] = e[3] - e[2];
+  *reinterpret_cast<f2*>(send + r * W + C + 2 * q) = p;
+  *reinterpret_cast<f2*>(keep1 + r * (C / 2) + 2 * q) = m;
+}
+
+// Mode A for other even C: one lane per column pair (2 elements), Philox word chosen per element.
+__global__ __launch_bounds__(kBlock) void k_mask_cols2(const float* __restrict__ a, float* __restrict__ send,
+                                                       float* __restrict__ keep0, float* __restrict__ keep1,
+                                                       long long R, long long C, uint64_t seed, uint64_t ctr0) {
+  const long long g = (long long)blockIdx.x * kBlock + threadIdx.x;
+  const long long h = C / 2;
+  if (g >= R * h) return;
+  const long long r = g / h, j = g - r * h;
+  const long long i = 2 * g;   // element index of a[r, 2j]; i % 4 is 0 or 2
+  float u[4];
+  draw4(seed, ctr0 + (uint64_t)(i >> 2), u);
+  const int w = (int)(i & 3);
+  const float x0 = a[i], x1 = a[i + 1];
+  const float e0 = u[w] * x0, e1 = u[w + 1] * x1;
+  const long long W = C + h;
+  send[r * W + 2 * j] = x0 + e0;
+  send[r * W + 2 * j + 1] = x1 + e1;
+  keep0[i] = x0 - e0;
+  keep0[i + 1] = x1 - e1;
+  send[r * W + C + j] = e0 + e1;
+  keep1[r * h + j] = e1 - e0;
+}
+
+// Mode B, b [K, N] with K even: lane g owns columns 4q..4q+3 of rows 2j and 2j+1 (N % 4 == 0) or
+// one column (general N). Element index of b[r, c] is r*N + c.
+// send [3K/2, N] = [b/2 - f ; f_even - f_odd], keep0 [K, N] = b/2 + f, keep1 [K/2, N] = f_odd + f_even.
+template <int V>
+__global__ __launch_bounds__(kBlock) void k_mask_rows(const float* __restrict__ b, float* __restrict__ send,
+                                                      float* __restrict__ keep0, float* __restrict__ keep1,
+                                                      long long K, long long N, uint64_t seed, uint64_t ctr0) {
+  const long long g = (long long)blockIdx.x * kBlock + threadIdx.x;
+  const long long nq = N / V;
+  if (g >= (K / 2) * nq) return;
+  const long long j = g / nq, q = g - j * nq;
+  const long long ie = 2 * j * N + V * q, io = ie + N;   // a[2j, Vq], a[2j+1, Vq]
+  float ue[4], uo[4];
+  draw4(seed, ctr0 + (uint64_t)(ie >> 2), ue);
+  draw4(seed, ctr0 + (uint64_t)(io >> 2), uo);
+  float xe[V], xo[V];
+  if (V == 4) {
+    const f4 ve = __builtin_nontemporal_load(reinterpret_cast<const f4*>(b + ie));
+    const f4 vo = __builtin_nontemporal_load(reinterpret_cast<const f4*>(b + io));
+#pragma unroll
+    for (int t = 0; t < V; ++t) { xe[t] = ve[t]; xo[t] = vo[t]; }
+  } else {
+    xe[0] = b[ie];
+    xo[0] = b[io];
+  }
+  float se[V], so[V], ke[V], ko[V], sd[V], kd[V];
+#pragma unroll
+  for (int t = 0; t < V; ++t) {
+    const float fe = ue[V == 4 ? t : (int)(ie & 3)] * xe[t];
+    const float fo = uo[V == 4 ? t : (int)(io & 3)] * xo[t];
+    const float he = xe[t] / 2.0f, ho = xo[t] / 2.0f;
+    se[t] = he - fe;
+    so[t] = ho - fo;
+    ke[t] = he + fe;
+    ko[t] = ho + fo;
+    sd[t] = fe - fo;
+    kd[t] = fo + fe;
+  }
+  const long long idf = K * N + j * N + V * q;   // row K + j of send
+  const long long ik = j * N + V * q;            // row j of keep1
+  if (V == 4) {
+    *reinterpret_cast<f4*>(send + ie) = f4{se[0], se[1], se[2], se[3]};
+    *reinterpret_cast<f4*>(send + io) = f4{so[0], so[1], so[2], so[3]};
+    *reinterpret_cast<f4*>(keep0 + ie) = f4{ke[0], ke[1], ke[2], ke[3]};
+    *reinterpret_cast<f4*>(keep0 + io) = f4{ko[0], ko[1], ko[2], ko[3]};
+    *reinterpret_cast<f4*>(send + idf) = f4{sd[0], sd[1], sd[2], sd[3]};
+    *reinterpret_cast<f4*>(keep1 + ik) = f4{kd[0], kd[1], kd[2], kd[3]};
+  } else {
+    send[ie] = se[0];
+    send[io] = so[0];
+    keep0[ie] = ke[0];
+    keep0[io] = ko[0];
+    send[idf] = sd[0];
+    keep1[ik] = kd[0];
+  }
+}
+
+unsigned grid_for(long long lanes) { return (unsigned)((lanes + kBlock - 1) / kBlock); }
+
+bool lanes_ok(long long lanes) { return lanes / kBlock < (1ll << 31); }
+
+}  // namespace
+}  // namespace efl
+
+using namespace efl;
+
+EFL_API int efl_ss_noise(const float* x, float* out0, float* out1, int64_t n, int op, uint64_t seed,
+                         uint64_t ctr0, float divisor, void* stream) {
+  if (n < 0) { set_error("negative element count"); return EFL_E_INVALID_ARGUMENT; }
+  if (op < 0 || op > 2) { set_error("efl_ss_noise: op must be 0, 1 or 2"); return EFL_E_INVALID_ARGUMENT; }
+  if (n == 0) return EFL_OK;
+  if (!x || !out0 || (op != 0 && !out1)) { set_error("null buffer"); return EFL_E_INVALID_ARGUMENT; }
+  if (!aligned(x, 16) || !aligned(out0, 16) || (op != 0 && !aligned(out1, 16))) {
+    set_error("efl_ss_noise: buffers must be 16-byte aligned");
+    return EFL_E_INVALID_ARGUMENT;
+  }
+  if (!(divisor == divisor) || divisor == 0.0f) { set_error("efl_ss_noise: divisor must be non-zero"); return EFL_E_INVALID_ARGUMENT; }
+  const long long lanes = (n + 3) / 4;
+  if (!lanes_ok(lanes)) { set_error("efl_ss_noise: tensor too large"); return EFL_E_INVALID_ARGUMENT; }
+  hipStream_t s = (hipStream_t)stream;
+  const int div = divisor != 1.0f;
+  switch (op) {
+    case 0: k_noise<0><<<grid_for(lanes), kBlock, 0, s>>>(x, out0, out1, n, seed, ctr0, divisor, div); break;
+    case 1: k_noise<1><<<grid_for(lanes), kBlock, 0, s>>>(x, out0, out1, n, seed, ctr0, divisor, div); break;
+    default: k_noise<2><<<grid_for(lanes), kBlock, 0, s>>>(x, out0, out1, n, seed, ctr0, divisor, div); break;
+  }
+  return hip_status(hipGetLastError(), "efl_ss_noise");
+}
+
+EFL_API int efl_ss_mask_cols(const float* a, float* send, float* keep0, float* keep1, int64_t rows,
+                             int64_t cols, uint64_t seed, uint64_t ctr0, void* stream) {
+  if (rows < 0 || cols < 0 || (cols & 1)) {
+    set_error("secret_sharing mode A: the columns of a must be even, got [%lld, %lld]", (long long)rows, (long long)cols);
+    return EFL_E_INVALID_ARGUMENT;
+  }
+  if (rows == 0 || cols == 0) return EFL_OK;
+  if (!a || !send || !keep0 || !keep1) { set_error("null buffer"); return EFL_E_INVALID_ARGUMENT; }
+  hipStream_t s = (hipStream_t)stream;
+  const bool v4 = cols % 8 == 0 && aligned(a, 16) && aligned(send, 16) && aligned(keep0, 16) && aligned(keep1, 8);
+  const long long lanes = v4 ? rows * (cols / 4) : rows * (cols / 2);
+  if (!lanes_ok(lanes)) { set_error("efl_ss_mask_cols: tensor too large"); return EFL_E_INVALID_ARGUMENT; }
+  if (v4) k_mask_cols4<<<grid_for(lanes), kBlock, 0, s>>>(a, send, keep0, keep1, rows, cols, seed, ctr0);
+  else k_mask_cols2<<<grid_for(lanes), kBlock, 0, s>>>(a, send, keep0, keep1, rows, cols, seed, ctr0);
+  return hip_status(hipGetLastError(), "efl_ss_mask_cols");
+}
+
+EFL_API int efl_ss_mask_rows(const float* b, float* send, float* keep0, float* keep1, int64_t rows,
+                             int64_t cols, uint64_t seed, uint64_t ctr0, void* stream) {
+  if (rows < 0 || cols < 0 || (rows & 1)) {
+    set_error("secret_sharing mode B: the rows of b must be even, got [%lld, %lld]", (long long)rows, (long long)cols);
+    return EFL_E_INVALID_ARGUMENT;
+  }
+  if (rows == 0 || cols == 0) return EFL_OK;
+  if (!b || !send || !keep0 || !keep1) { set_error("null buffer"); return EFL_E_INVALID_ARGUMENT; }
+  hipStream_t s = (hipStream_t)stream;
+  const bool v4 = cols % 4 == 0 && aligned(b, 16) && aligned(send, 16) && aligned(keep0, 16) && aligned(keep1, 16);
+  const long long lanes = (rows / 2) * (v4 ? cols / 4 : cols);
+  if (!lanes_ok(lanes)) { set_error("efl_ss_mask_rows: tensor too large"); return EFL_E_INVALID_ARGUMENT; }
+  if (v4) k_mask_rows<4><<<grid_for(lanes), kBlock, 0, s>>>(b, send, keep0, keep1, rows, cols, seed, ctr0);
+  else k_mask_rows<1><<<grid_for(lanes), kBlock, 0, s>>>(b, send, keep0, keep1, rows, cols, seed, ctr0);
+  return hip_status(hipGetLastError(), "efl_ss_mask_rows");
+}

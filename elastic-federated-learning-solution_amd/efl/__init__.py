@@ -3,6 +3,7 @@
 Public names mirror efls-train/python/efl (exporter registry, efl/__init__.py:47):
   efl.paillier.fixedpoint.{encode, decode, Tensor}, efl.paillier.{Keypair, Tensor}
   efl.Communicator (gRPC TrainerService, pre-send/post-recv hooks), efl.privacy.FixedPointHook
+  efl.secret_sharing.{matmul, Dense, dense, share, reveal}
   efl.HexTensor (the DT_STRING stand-in), efl.lib.ops (the `fed_ops` namespace)
 The kernels live in libefl_hip.so (C ABI: include/efl_hip.h); there is no CPU fallback.
 """
@@ -14,6 +15,7 @@ from efl.privacy import encryptor_utils
 from efl.privacy import paillier
 from efl.privacy import paillier_cipher
 from efl.privacy import paillier_layer
+from efl.privacy import secret_sharing
 from efl.privacy.hex_tensor import HexTensor
 from efl.framework import communicator
 from efl.framework import encrypt_hook

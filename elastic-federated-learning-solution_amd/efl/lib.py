@@ -41,6 +41,9 @@ _SIGS = {
     "efl_fxp_decode_hex": ([_vp, _vp, _vp, _vp, _i32, _i64, _i32, _vp, _vp], _i32),
     "efl_fxp_encode_batched": ([_vp, _i32, _vp, _vp, _vp, _i64, _i64, _i32, _vp], _i32),
     "efl_fxp_decode_batched": ([_vp, _vp, _vp, _i32, _vp, _i64, _i64, _i32, _vp], _i32),
+    "efl_ss_noise": ([_vp, _vp, _vp, _i64, _i32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_float, _vp], _i32),
+    "efl_ss_mask_cols": ([_vp, _vp, _vp, _vp, _i64, _i64, ctypes.c_uint64, ctypes.c_uint64, _vp], _i32),
+    "efl_ss_mask_rows": ([_vp, _vp, _vp, _vp, _i64, _i64, ctypes.c_uint64, ctypes.c_uint64, _vp], _i32),
 }
 for _name, (_args, _ret) in _SIGS.items():
     _f = getattr(_lib, _name)

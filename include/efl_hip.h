@@ -252,6 +252,28 @@ int efl_hex_parse(const char* chars, const int64_t* offsets, int limbs_per_elem,
 int efl_pl_to_int64(const uint32_t* magnitude, int limbs_per_elem, const int8_t* negative,
                     int64_t* out, int64_t n, void* stream);
 
+/* ---- Secret-sharing masks -------------------------------------------------
+ * Replace the per-element float work of efls-train/python/efl/privacy/secret_sharing.py, whose
+ * noise is generate_suitable_noise(t) = tf.random.uniform(shape(t)) * t (:26-27). The uniform is
+ * TF's construction (Philox4x32-10, Uint32ToFloat): element i of a call takes word i % 4 of Philox
+ * block (ctr0 + i / 4) under key `seed`; a caller advances ctr0 by ceil(n / 4) per call. fp32 only
+ * (tf.random.uniform's default dtype). Buffers are device memory, row-major, caller-allocated. */
+/* n = U * x / divisor, and: op 0: out0 = n; op 1 (share(), :158-168): out0 = n (sent),
+ * out1 = x - n (kept); op 2 (SecretSharingDense noise_divisor, :137-143): out0 = x - n (sent),
+ * out1 = x + n (kept). 16-byte aligned buffers. */
+int efl_ss_noise(const float* x, float* out0, float* out1, int64_t n, int op, uint64_t seed,
+                 uint64_t ctr0, float divisor, void* stream);
+/* _matmul mode A side (:30-41), a [rows, cols], cols even, e = U * a:
+ * send [rows, 3*cols/2] = [a + e | e[:, ::2] + e[:, 1::2]], keep0 [rows, cols] = a - e,
+ * keep1 [rows, cols/2] = e[:, 1::2] - e[:, ::2]. */
+int efl_ss_mask_cols(const float* a, float* send, float* keep0, float* keep1, int64_t rows,
+                     int64_t cols, uint64_t seed, uint64_t ctr0, void* stream);
+/* _matmul mode B side (:42-53), b [rows, cols], rows even, f = U * b:
+ * send [3*rows/2, cols] = [b/2 - f ; f[::2] - f[1::2]], keep0 [rows, cols] = b/2 + f,
+ * keep1 [rows/2, cols] = f[1::2] + f[::2]. */
+int efl_ss_mask_rows(const float* b, float* send, float* keep0, float* keep1, int64_t rows,
+                     int64_t cols, uint64_t seed, uint64_t ctr0, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,93 @@
+#!/usr/bin/env python3
+"""Secret-sharing masks on one MI355X: the per-element kernels of
+csrc/mask.hip on a 256 MiB fp32 tensor ([65536, 1024], the BASELINE config-2 shape), timed with HIP
+events on the launch stream, against their HBM roofline, beside the numpy oracle (the TF op chain
+restated: uniform, mul, slices, adds, concat) on a bounded CPU sample. One JSON line per kernel.
+
+Algorithmic bytes per fp32 element (read x once, write every output once):
+  noise (op 0)            4 + 4            =  8 B
+  share (op 1), weight (op 2)  4 + 4 + 4   = 12 B
+  mask_cols (mode A)      4 + 6 + 4 + 2    = 16 B  (send 3/2, keep a - e, keep 1/2)
+  mask_rows (mode B)      4 + 6 + 4 + 2    = 16 B
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "elastic-federated-learning-solution_amd"))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import efl  # noqa: E402
+
+PEAK_GBS = 8000.0
+ap = argparse.ArgumentParser()
+ap.add_argument("--rows", type=int, default=65536)
+ap.add_argument("--cols", type=int, default=1024)
+ap.add_argument("--steps", type=int, default=50)
+ap.add_argument("--no-cpu-baseline", action="store_true")
+args = ap.parse_args()
+
+dev = efl.lib.require_gpu()
+lib = efl.lib.raw()
+R, C = args.rows, args.cols
+n = R * C
+x = torch.randn(R, C, device=dev, generator=torch.Generator(device=dev).manual_seed(0))
+o0, o1 = torch.empty_like(x), torch.empty_like(x)
+send_c = torch.empty(R, C * 3 // 2, device=dev)
+k1_c = torch.empty(R, C // 2, device=dev)
+send_r = torch.empty(R * 3 // 2, C, device=dev)
+k1_r = torch.empty(R // 2, C, device=dev)
+s = torch.cuda.current_stream()
+sh = s.cuda_stream
+xp, p0, p1 = x.data_ptr(), o0.data_ptr(), o1.data_ptr()
+
+cases = {
+    "noise": (8, lambda: lib.efl_ss_noise(xp, p0, p1, n, 0, 7, 0, 1.0, sh)),
+    "share": (12, lambda: lib.efl_ss_noise(xp, p0, p1, n, 1, 7, 0, 1.0, sh)),
+    "weight_noise": (12, lambda: lib.efl_ss_noise(xp, p0, p1, n, 2, 7, 0, 2.0, sh)),
+    "mask_cols": (16, lambda: lib.efl_ss_mask_cols(xp, send_c.data_ptr(), p0, k1_c.data_ptr(), R, C, 7, 0, sh)),
+    "mask_rows": (16, lambda: lib.efl_ss_mask_rows(xp, send_r.data_ptr(), p0, k1_r.data_ptr(), R, C, 7, 0, sh)),
+}
+
+
+def cpu_sample(name, rows=1024):
+    """The oracle (numpy, the reference's op chain) on the first `rows` rows; GiB/s of input."""
+    from oracle import mask
+    xs = x[:rows].cpu().numpy()
+    fn = {"noise": lambda: mask.noise(xs, 7, 0, 0), "share": lambda: mask.noise(xs, 7, 0, 1),
+          "weight_noise": lambda: mask.noise(xs, 7, 0, 2, 2.0),
+          "mask_cols": lambda: mask.mask_cols(xs, 7, 0), "mask_rows": lambda: mask.mask_rows(xs, 7, 0)}[name]
+    fn()
+    reps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < 2.0:
+        fn()
+        reps += 1
+    dt = (time.perf_counter() - t0) / reps
+    return {"value": round(xs.nbytes / dt / 2**30, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"[{rows}, {C}] fp32 slice, numpy oracle/mask.py (uniform + elementwise + concat), {reps} reps"}
+
+
+for name, (bpe, fn) in cases.items():
+    for _ in range(5):
+        efl.lib.check(fn())
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(args.steps):
+        fn()
+    e1.record(s)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / args.steps
+    gbs = bpe * n / (ms * 1e-3) / 1e9
+    line = {"kernel": name, "elements": n, "shape": [R, C], "ms": round(ms, 4),
+            "GiB_per_s_plaintext": round(4 * n / (ms * 1e-3) / 2**30, 2),
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_GBS, "unit": "GB/s",
+                         "frac": round(gbs / PEAK_GBS, 4), "bytes_per_elem": bpe}}
+    if not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_sample(name)
+    print(json.dumps(line), flush=True)
