@@ -420,16 +420,17 @@ __global__ __launch_bounds__(kBlock) void k_decode_hex(const char* chars, const 
 // ------------------------------------------------------------------------------------------
 
 // Per-direction launch shape of the fp32 kernels. Defaults: the fastest shape of the interleaved
-// sweep on MI355X (tools/sweep_fxp.py -> profiles/r01/sweep_shapes.jsonl): pair layout, one tile
-// of 128 lanes per workgroup, nontemporal LOADS (the once-read stream), plain stores. Plain vs
-// nontemporal stores were within noise for encode; nontemporal loads gained ~5 % on decode.
+// sweep on MI355X (tools/sweep_fxp.py -> profiles/r01/sweep_*.jsonl), pair layout, one tile per
+// workgroup. Decode: 128 lanes, nontemporal loads (+5 % over plain loads). Encode: 256 lanes,
+// nontemporal loads AND stores: 0.199 vs 0.211 ms for 128 lanes / plain stores on the current
+// kernel (profiles/r01/sweep_encode_nt.jsonl, tools/enc_probe.hip shows the same on the bare mix).
 struct Shape {
   std::atomic<int> variant;   // 0 pair, 1 quad
   std::atomic<int> block;     // 128, 256, 512
   std::atomic<int> k;         // units per lane per tile: 1, 2
   std::atomic<int> nt;        // bit0 nontemporal loads, bit1 nontemporal stores
 };
-Shape g_shape[2] = {{{0}, {128}, {1}, {1}}, {{0}, {128}, {1}, {1}}};
+Shape g_shape[2] = {{{0}, {256}, {1}, {3}}, {{0}, {128}, {1}, {1}}};
 std::atomic<int> g_grid_cap{0};   // 0: one tile per workgroup; else max workgroups
 constexpr int kEnc = 0, kDec = 1;
 
