@@ -432,6 +432,8 @@ struct Shape {
 };
 Shape g_shape[2] = {{{0}, {256}, {1}, {3}}, {{0}, {128}, {1}, {1}}};
 std::atomic<int> g_grid_cap{0};   // 0: one tile per workgroup; else max workgroups
+// NT mask of the fp32 batched encode (efl_fxp_tune kind 9): 1 nontemporal loads, 3 loads + stores
+std::atomic<int> g_batch_enc_nt{3};
 constexpr int kEnc = 0, kDec = 1;
 
 template <class Op, int B, int K, int NT>
@@ -538,6 +540,10 @@ EFL_API const char* efl_version(void) { return "efl-hip 0.1.0 (gfx950)"; }
 EFL_API const char* efl_last_error(void) { return t_err.c_str(); }
 
 EFL_API int efl_fxp_tune(int kind, int value) {
+  if (kind == 9) {
+    if (value != 1 && value != 3) return EFL_E_INVALID_ARGUMENT;
+    return g_batch_enc_nt.exchange(value);
+  }
   if (kind == 8) {
     if (value < 0) return EFL_E_INVALID_ARGUMENT;
     return g_grid_cap.exchange(value);
@@ -673,7 +679,10 @@ EFL_API int efl_fxp_encode_batched(const void* const* xs, int dtype, int64_t* co
   const int f = decrease_precision ? 1 : 0;
   hipError_t e;
   switch (dtype) {
-    case EFL_DT_FLOAT: e = launch_batched<EncF32Pair, 1>(xs, d0, d1, nn, count, max_n, f, s); break;
+    case EFL_DT_FLOAT:
+      e = g_batch_enc_nt.load() == 3 ? launch_batched<EncF32Pair, 3>(xs, d0, d1, nn, count, max_n, f, s)
+                                     : launch_batched<EncF32Pair, 1>(xs, d0, d1, nn, count, max_n, f, s);
+      break;
     case EFL_DT_DOUBLE: e = launch_batched<EncF64Pair, 1>(xs, d0, d1, nn, count, max_n, f, s); break;
     case EFL_DT_INT8: e = launch_batched<EncIntPair<signed char, c2>, 1>(xs, d0, d1, nn, count, max_n, f, s); break;
     case EFL_DT_INT16: e = launch_batched<EncIntPair<short, s2>, 1>(xs, d0, d1, nn, count, max_n, f, s); break;

@@ -29,6 +29,16 @@ namespace {
 
 using pl::philox;
 
+// EFL_MASK_NT=1 builds nontemporal stores (tuning variant; the default is chosen by measurement)
+#ifndef EFL_MASK_NT
+#define EFL_MASK_NT 0
+#endif
+template <class T>
+__device__ __forceinline__ void stv(T* p, T v) {
+  if constexpr (EFL_MASK_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
 __device__ __forceinline__ float u01(uint32_t w) {
   return __uint_as_float(0x3f800000u | (w & 0x7fffffu)) - 1.0f;
 }
@@ -68,8 +78,8 @@ __global__ __launch_bounds__(kBlock) void k_noise(const float* __restrict__ x, f
       if (OP == 1) { a[j] = nz; b[j] = v[j] - nz; }
       if (OP == 2) { a[j] = v[j] - nz; b[j] = v[j] + nz; }
     }
-    reinterpret_cast<f4*>(o0)[g] = a;
-    if (OP != 0) reinterpret_cast<f4*>(o1)[g] = b;
+    stv(reinterpret_cast<f4*>(o0) + g, a);
+    if (OP != 0) stv(reinterpret_cast<f4*>(o1) + g, b);
   } else {
     for (int j = 0; j < 4 && i0 + j < n; ++j) {
       const float xv = x[i0 + j];
@@ -103,15 +113,15 @@ __global__ __launch_bounds__(kBlock) void k_mask_cols4(const float* __restrict__
     k[j] = v[j] - e[j];
   }
   const long long W = C + C / 2;
-  *reinterpret_cast<f4*>(send + r * W + 4 * q) = s;
-  reinterpret_cast<f4*>(keep0)[g] = k;
+  stv(reinterpret_cast<f4*>(send + r * W + 4 * q), s);
+  stv(reinterpret_cast<f4*>(keep0) + g, k);
   f2 p, m;
   p[0] = e[0] + e[1];
   p[1] = e[2] + e[3];
   m[0] = e[1] - e[0];
   m[1] = e[3] - e[2];
-  *reinterpret_cast<f2*>(send + r * W + C + 2 * q) = p;
-  *reinterpret_cast<f2*>(keep1 + r * (C / 2) + 2 * q) = m;
+  stv(reinterpret_cast<f2*>(send + r * W + C + 2 * q), p);
+  stv(reinterpret_cast<f2*>(keep1 + r * (C / 2) + 2 * q), m);
 }
 
 // Mode A for other even C: one lane per column pair (2 elements), Philox word chosen per element.
@@ -178,12 +188,12 @@ __global__ __launch_bounds__(kBlock) void k_mask_rows(const float* __restrict__ 
   const long long idf = K * N + j * N + V * q;   // row K + j of send
   const long long ik = j * N + V * q;            // row j of keep1
   if (V == 4) {
-    *reinterpret_cast<f4*>(send + ie) = f4{se[0], se[1], se[2], se[3]};
-    *reinterpret_cast<f4*>(send + io) = f4{so[0], so[1], so[2], so[3]};
-    *reinterpret_cast<f4*>(keep0 + ie) = f4{ke[0], ke[1], ke[2], ke[3]};
-    *reinterpret_cast<f4*>(keep0 + io) = f4{ko[0], ko[1], ko[2], ko[3]};
-    *reinterpret_cast<f4*>(send + idf) = f4{sd[0], sd[1], sd[2], sd[3]};
-    *reinterpret_cast<f4*>(keep1 + ik) = f4{kd[0], kd[1], kd[2], kd[3]};
+    stv(reinterpret_cast<f4*>(send + ie), f4{se[0], se[1], se[2], se[3]});
+    stv(reinterpret_cast<f4*>(send + io), f4{so[0], so[1], so[2], so[3]});
+    stv(reinterpret_cast<f4*>(keep0 + ie), f4{ke[0], ke[1], ke[2], ke[3]});
+    stv(reinterpret_cast<f4*>(keep0 + io), f4{ko[0], ko[1], ko[2], ko[3]});
+    stv(reinterpret_cast<f4*>(send + idf), f4{sd[0], sd[1], sd[2], sd[3]});
+    stv(reinterpret_cast<f4*>(keep1 + ik), f4{kd[0], kd[1], kd[2], kd[3]});
   } else {
     send[ie] = se[0];
     send[io] = so[0];

@@ -17,6 +17,8 @@ import efl  # noqa: E402
 SLICES, ELEMS = 4096, 16384
 dev = efl.lib.require_gpu()
 lib = efl.lib.raw()
+if os.environ.get("EFL_BATCH_ENC_NT"):   # A/B of the batched encode's store flags (efl_fxp_tune 9)
+    lib.efl_fxp_tune(9, int(os.environ["EFL_BATCH_ENC_NT"]))
 g = torch.Generator(device=dev).manual_seed(1)
 # separate allocations per slice (realistic: embedding rows live in different tensors)
 xs = [torch.randn(128, 128, device=dev, generator=g) * 0.01 for _ in range(SLICES)]
