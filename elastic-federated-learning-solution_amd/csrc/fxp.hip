@@ -112,8 +112,12 @@ __device__ __forceinline__ unsigned long long dec_any_bits(long long M, long lon
 }
 
 // ------------------------------------------------------------------------------------------
-// memory helpers (NT bit 0: nontemporal loads, bit 1: nontemporal stores)
+// memory helpers (NT bit 0: nontemporal loads, bit 1: nontemporal stores, bit 2 (with bit 1):
+// 16-B stores as `global_store_dwordx4 ... nt sc1`, which also drop the line from the XCD's L2
+// (MI355X_MICROARCH.md, store flavours) so the next kernel inherits no dirty encode output)
 // ------------------------------------------------------------------------------------------
+
+typedef int i4 __attribute__((ext_vector_type(4)));
 
 template <int NT, class T>
 __device__ __forceinline__ T ld(const T* p) {
@@ -122,8 +126,16 @@ __device__ __forceinline__ T ld(const T* p) {
 }
 template <int NT, class T>
 __device__ __forceinline__ void st(T* p, T v) {
-  if constexpr (NT & 2) __builtin_nontemporal_store(v, p);
-  else *p = v;
+  if constexpr ((NT & 4) && sizeof(T) == 16) {
+    const i4 w = __builtin_bit_cast(i4, v);
+    // The compiler's hazard recognizer does not see a store inside inline asm: a VALU write to
+    // the data VGPRs right after a >8-byte store needs a wait state on gfx950, so pad it here.
+    asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" ::"v"(p), "v"(w) : "memory");
+  } else if constexpr (NT & 2) {
+    __builtin_nontemporal_store(v, p);
+  } else {
+    *p = v;
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -422,18 +434,20 @@ __global__ __launch_bounds__(kBlock) void k_decode_hex(const char* chars, const 
 // Per-direction launch shape of the fp32 kernels. Defaults: the fastest shape of the interleaved
 // sweep on MI355X (tools/sweep_fxp.py -> profiles/r01/sweep_*.jsonl), pair layout, one tile per
 // workgroup. Decode: 128 lanes, nontemporal loads (+5 % over plain loads). Encode: 256 lanes,
-// nontemporal loads AND stores: 0.199 vs 0.211 ms for 128 lanes / plain stores on the current
-// kernel (profiles/r01/sweep_encode_nt.jsonl, tools/enc_probe.hip shows the same on the bare mix).
+// nontemporal loads and `nt sc1` stores (NT mask 7): in the bench step 0.197 vs 0.209 ms for
+// 128 lanes / plain stores, and 1.5-3 % below plain `nt` stores (profiles/r01/ab_*.json,
+// tools/enc_probe.hip on the bare mix); it also takes decode's time down (no inherited dirty lines).
 struct Shape {
   std::atomic<int> variant;   // 0 pair, 1 quad
   std::atomic<int> block;     // 128, 256, 512
   std::atomic<int> k;         // units per lane per tile: 1, 2
   std::atomic<int> nt;        // bit0 nontemporal loads, bit1 nontemporal stores
 };
-Shape g_shape[2] = {{{0}, {256}, {1}, {3}}, {{0}, {128}, {1}, {1}}};
+Shape g_shape[2] = {{{0}, {256}, {1}, {7}}, {{0}, {128}, {1}, {1}}};
 std::atomic<int> g_grid_cap{0};   // 0: one tile per workgroup; else max workgroups
-// NT mask of the fp32 batched encode (efl_fxp_tune kind 9): 1 nontemporal loads, 3 loads + stores
-std::atomic<int> g_batch_enc_nt{3};
+// NT mask of the fp32 batched encode (efl_fxp_tune kind 9): 1 nontemporal loads, 3 loads + stores,
+// 7 loads + `nt sc1` stores (default, as the streaming encode)
+std::atomic<int> g_batch_enc_nt{7};
 constexpr int kEnc = 0, kDec = 1;
 
 template <class Op, int B, int K, int NT>
@@ -454,6 +468,7 @@ hipError_t launch_nt(int nt, const typename Op::Args& a, long long nunits, hipSt
     case 1: return launch_k<Op, B, K, 1>(a, nunits, s);
     case 2: return launch_k<Op, B, K, 2>(a, nunits, s);
     case 3: return launch_k<Op, B, K, 3>(a, nunits, s);
+    case 7: return launch_k<Op, B, K, 7>(a, nunits, s);
     default: return launch_k<Op, B, K, 0>(a, nunits, s);
   }
 }
@@ -541,7 +556,7 @@ EFL_API const char* efl_last_error(void) { return t_err.c_str(); }
 
 EFL_API int efl_fxp_tune(int kind, int value) {
   if (kind == 9) {
-    if (value != 1 && value != 3) return EFL_E_INVALID_ARGUMENT;
+    if (value != 1 && value != 3 && value != 7) return EFL_E_INVALID_ARGUMENT;
     return g_batch_enc_nt.exchange(value);
   }
   if (kind == 8) {
@@ -558,7 +573,7 @@ EFL_API int efl_fxp_tune(int kind, int value) {
       if (value != 1 && value != 2) return EFL_E_INVALID_ARGUMENT;
       return sh.k.exchange(value);
     case 2:
-      if (value < 0 || value > 3) return EFL_E_INVALID_ARGUMENT;
+      if (value < 0 || (value > 3 && value != 7)) return EFL_E_INVALID_ARGUMENT;
       return sh.nt.exchange(value);
     default:
       if (value != 128 && value != 256 && value != 512) return EFL_E_INVALID_ARGUMENT;
@@ -680,8 +695,11 @@ EFL_API int efl_fxp_encode_batched(const void* const* xs, int dtype, int64_t* co
   hipError_t e;
   switch (dtype) {
     case EFL_DT_FLOAT:
-      e = g_batch_enc_nt.load() == 3 ? launch_batched<EncF32Pair, 3>(xs, d0, d1, nn, count, max_n, f, s)
-                                     : launch_batched<EncF32Pair, 1>(xs, d0, d1, nn, count, max_n, f, s);
+      switch (g_batch_enc_nt.load()) {
+        case 7: e = launch_batched<EncF32Pair, 7>(xs, d0, d1, nn, count, max_n, f, s); break;
+        case 3: e = launch_batched<EncF32Pair, 3>(xs, d0, d1, nn, count, max_n, f, s); break;
+        default: e = launch_batched<EncF32Pair, 1>(xs, d0, d1, nn, count, max_n, f, s); break;
+      }
       break;
     case EFL_DT_DOUBLE: e = launch_batched<EncF64Pair, 1>(xs, d0, d1, nn, count, max_n, f, s); break;
     case EFL_DT_INT8: e = launch_batched<EncIntPair<signed char, c2>, 1>(xs, d0, d1, nn, count, max_n, f, s); break;

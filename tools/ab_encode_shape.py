@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """A/B of the encode launch shape inside the bench step (encode then decode, back to back, no sync
 between steps), interleaved rounds in one process so box and clock drift land on both arms.
-Arm "old": 128 lanes, nontemporal loads, plain stores. Arm "new" (default since): 256 lanes,
-nontemporal loads and stores. Prints one JSON line: median step ms and per-kernel ms per arm."""
+Arm "old": 128 lanes, nontemporal loads, plain stores. Arm "nt": 256 lanes, nontemporal loads and
+stores. Arm "new" (the default): 256 lanes, nontemporal loads, `nt sc1` stores. Prints one JSON line: median step ms and per-kernel ms per arm."""
 import json
 import os
 import sys
@@ -24,7 +24,7 @@ y = torch.empty_like(x)
 s = torch.cuda.current_stream()
 sh = s.cuda_stream
 # arm = (encode block, encode NT mask, decode block, decode NT mask); AB_ARMS="name:b,nt,b,nt;..."
-ARMS = {"old": (128, 1, 128, 1), "new": (256, 3, 128, 1)}
+ARMS = {"old": (128, 1, 128, 1), "nt": (256, 3, 128, 1), "new": (256, 7, 128, 1)}
 if os.environ.get("AB_ARMS"):
     ARMS = {a.split(":")[0]: tuple(int(v) for v in a.split(":")[1].split(","))
             for a in os.environ["AB_ARMS"].split(";")}

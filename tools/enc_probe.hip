@@ -71,6 +71,30 @@ __global__ __launch_bounds__(256) void k_pair_nt(const f2* __restrict__ x, ll2* 
   __builtin_nontemporal_store(mk(v.x, v.y, 1), E + u);
 }
 
+// V6: stores with explicit cache-policy bits (gfx950 global_store_dwordx4 ... off <bits>)
+typedef int i4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st16_sc1(ll2* p, ll2 v) {
+  i4 w = __builtin_bit_cast(i4, v);
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(p), "v"(w) : "memory");
+}
+__device__ __forceinline__ void st16_sc0sc1(ll2* p, ll2 v) {
+  i4 w = __builtin_bit_cast(i4, v);
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" :: "v"(p), "v"(w) : "memory");
+}
+__device__ __forceinline__ void st16_ntsc1(ll2* p, ll2 v) {
+  i4 w = __builtin_bit_cast(i4, v);
+  asm volatile("global_store_dwordx4 %0, %1, off nt sc1" :: "v"(p), "v"(w) : "memory");
+}
+template <int MODE>
+__global__ __launch_bounds__(256) void k_pair_bits(const f2* __restrict__ x, ll2* __restrict__ M, ll2* __restrict__ E, long long nu) {
+  const long long u = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (u >= nu) return;
+  const f2 v = __builtin_nontemporal_load(x + u);
+  if (MODE == 0) { st16_sc1(M + u, mk(v.x, v.y, 0)); st16_sc1(E + u, mk(v.x, v.y, 1)); }
+  if (MODE == 1) { st16_sc0sc1(M + u, mk(v.x, v.y, 0)); st16_sc0sc1(E + u, mk(v.x, v.y, 1)); }
+  if (MODE == 2) { st16_ntsc1(M + u, mk(v.x, v.y, 0)); st16_ntsc1(E + u, mk(v.x, v.y, 1)); }
+}
+
 // V5: all M of a workgroup tile, then all E (two phases, each one contiguous 4 KiB per block)
 __global__ __launch_bounds__(256) void k_pair_phase(const f2* __restrict__ x, ll2* __restrict__ M, ll2* __restrict__ E, long long nu) {
   const long long u = (long long)blockIdx.x * 256 + threadIdx.x;
@@ -102,9 +126,10 @@ struct Timed {
 int main(int argc, char** argv) {
   const long long n = argc > 1 ? atoll(argv[1]) : 65536LL * 1024;
   if (n <= 0 || n % 1024) return 2;
-  float* x;
+  float *x, *y;
   long long *M, *E;
   CHECK(hipMalloc(&x, n * 4));
+  CHECK(hipMalloc(&y, n * 4));
   CHECK(hipMalloc(&M, n * 8));
   CHECK(hipMalloc(&E, n * 8));
   CHECK(hipMemset(x, 0x3f, n * 4));
@@ -120,6 +145,17 @@ int main(int argc, char** argv) {
       {"pair2", b20, [&] { hipLaunchKernelGGL(k_pair2, dim3(nu / 512), dim3(256), 0, 0, (const f2*)x, (ll2*)M, (ll2*)E, nu); }, {}},
       {"pair_nt", b20, [&] { hipLaunchKernelGGL(k_pair_nt, dim3(nu / 256), dim3(256), 0, 0, (const f2*)x, (ll2*)M, (ll2*)E, nu); }, {}},
       {"pair_phase", b20, [&] { hipLaunchKernelGGL(k_pair_phase, dim3(nu / 256), dim3(256), 0, 0, (const f2*)x, (ll2*)M, (ll2*)E, nu); }, {}},
+      {"pair_sc1", b20, [&] { hipLaunchKernelGGL(k_pair_bits<0>, dim3(nu / 256), dim3(256), 0, 0, (const f2*)x, (ll2*)M, (ll2*)E, nu); }, {}},
+      {"pair_sc0sc1", b20, [&] { hipLaunchKernelGGL(k_pair_bits<1>, dim3(nu / 256), dim3(256), 0, 0, (const f2*)x, (ll2*)M, (ll2*)E, nu); }, {}},
+      {"pair_ntsc1", b20, [&] { hipLaunchKernelGGL(k_pair_bits<2>, dim3(nu / 256), dim3(256), 0, 0, (const f2*)x, (ll2*)M, (ll2*)E, nu); }, {}},
+      {"step_plain", 2 * b20, [&] { hipLaunchKernelGGL(k_pair<256>, dim3(nu / 256), dim3(256), 0, 0, (const f2*)x, (ll2*)M, (ll2*)E, nu);
+                                   if (efl_fxp_decode((const int64_t*)M, (const int64_t*)E, y, EFL_DT_FLOAT, n, n, 0, nullptr)) exit(3); }, {}},
+      {"step_nt", 2 * b20, [&] { hipLaunchKernelGGL(k_pair_nt, dim3(nu / 256), dim3(256), 0, 0, (const f2*)x, (ll2*)M, (ll2*)E, nu);
+                                if (efl_fxp_decode((const int64_t*)M, (const int64_t*)E, y, EFL_DT_FLOAT, n, n, 0, nullptr)) exit(3); }, {}},
+      {"step_sc1", 2 * b20, [&] { hipLaunchKernelGGL(k_pair_bits<0>, dim3(nu / 256), dim3(256), 0, 0, (const f2*)x, (ll2*)M, (ll2*)E, nu);
+                                 if (efl_fxp_decode((const int64_t*)M, (const int64_t*)E, y, EFL_DT_FLOAT, n, n, 0, nullptr)) exit(3); }, {}},
+      {"step_ntsc1", 2 * b20, [&] { hipLaunchKernelGGL(k_pair_bits<2>, dim3(nu / 256), dim3(256), 0, 0, (const f2*)x, (ll2*)M, (ll2*)E, nu);
+                                   if (efl_fxp_decode((const int64_t*)M, (const int64_t*)E, y, EFL_DT_FLOAT, n, n, 0, nullptr)) exit(3); }, {}},
       {"mask_mix", b16, [&] { hipLaunchKernelGGL(k_mask_mix, dim3(nq / 256), dim3(256), 0, 0, (const f4*)x, (f4*)M, (f4*)E, (f2*)(E + n / 2 + 1024), nq); }, {}},
       {"efl_encode", b20, [&] { if (efl_fxp_encode(x, EFL_DT_FLOAT, (int64_t*)M, (int64_t*)E, n, 0, nullptr)) exit(3); }, {}},
   };

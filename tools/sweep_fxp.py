@@ -25,7 +25,7 @@ y = torch.empty_like(x)
 s = torch.cuda.current_stream()
 sh = s.cuda_stream
 # the library's defaults (csrc/fxp.hip g_shape): read back by setting, then restored below
-_DEF = {0: ((0, 0), (1, 1), (2, 3), (3, 256)), 1: ((0, 0), (1, 1), (2, 1), (3, 128))}
+_DEF = {0: ((0, 0), (1, 1), (2, 7), (3, 256)), 1: ((0, 0), (1, 1), (2, 1), (3, 128))}
 DEFAULT = {d: {f: lib.efl_fxp_tune(2 * f + d, v) for f, v in _DEF[d]} for d in (0, 1)}
 for d in (0, 1):
     for f, v in DEFAULT[d].items():
