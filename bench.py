@@ -11,13 +11,21 @@ ConvertToFixedPoint (fp32 -> int64 mantissa + int64 exponent) followed by FixedP
 
 value = (N x 0.25 GiB) / (max over ranks of the time of K steps / K)        [GiB/s, weak scaling]
 Multi-GPU: every rank owns its own 256 MiB shard (the path is element-wise: no payload exchange);
-the only collective is the RCCL broadcast of the 32-byte key seed from rank 0 (timed apart).
+the only collective is the broadcast of the 32-byte key seed from rank 0 (timed apart): RCCL when
+every rank has its own GPU, gloo when ranks share one (efl.distributed.choose_backend).
 
-roofline: per-kernel average durations come from HIP events recorded around every launch on the
-stream the kernels run on, inside the timed region. Algorithmic bytes: 20 B/element per kernel
-(encode: 4 read + 16 written; decode: 16 read + 4 written), SURVEY.md §8(d).
-cpu_baseline: the reference CPU op restated (oracle/: encode loop + GMP mpf decode, TF-Shard-like
-contiguous blocks over host threads) timed on this box on the same tensor (rank 0, N = 1 only).
+The timed region holds nothing but the K steps (no events, no host work between launches).
+roofline: per-kernel average durations come from a second pass of K steps right after it, with HIP
+events recorded around every launch on the stream the kernels run on. Algorithmic bytes:
+20 B/element per kernel (encode: 4 read + 16 written; decode: 16 read + 4 written), SURVEY.md §8(d).
+Decode runs in the reference's TF-runtime rounding mode (FTZ, efl.lib.flush_denormal()).
+cpu_baseline: the reference CPU op (oracle/: the literal encode loop of fixed_point.cc:107-137 +
+the GMP mpf decode of :235-248, FTZ|DAZ like a TF threadpool thread, contiguous blocks like TF
+Shard over every usable host core) timed on this box on the same tensor (rank 0, N = 1 only).
+Extra keys at N = 1: "config3" (BASELINE config 3: 4096 x 64 KiB slices, one batched launch per
+direction, and the naive per-slice launches) and "pinned_path" (the north_star's rate including
+pinned H2D/D2H copies: efl.framework.host_pipeline over the same tensor, encrypt leg pinned fp32 ->
+pinned M+E, decrypt leg back).
 
     python bench.py --stage p      Stage P report (SURVEY.md §8(d) last row), one JSON line per key:
 Paillier encrypt (fresh randomness through the fixed-base table) and CRT decrypt of int64
@@ -29,6 +37,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -47,13 +56,35 @@ BYTES_PER_ELEM_KERNEL = 20     # each of encode / decode
 GIB = float(1 << 30)
 
 
+def usable_cores():
+    """Host cores this process may run on: the affinity mask, capped by a cgroup CPU quota
+    (cgroup v2 cpu.max) when one is set. Returns (count, how it was found)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    if quota is not None and math.ceil(quota) < aff:
+        return max(1, int(math.ceil(quota))), f"cgroup cpu.max quota {quota:g} CPUs (affinity {aff})"
+    return aff, f"sched_getaffinity: {aff} CPUs" + (f" (cgroup quota {quota:g})" if quota else "")
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--backend", choices=("nccl", "gloo"), default=None,
+                   help="process-group backend for N > 1 (default: nccl if every rank has a GPU)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-threads", type=int, default=int(os.environ.get("EFL_BENCH_CPU_THREADS", "16")))
+    p.add_argument("--no-extras", action="store_true", help="skip the config3 / pinned_path keys")
+    p.add_argument("--cpu-threads", type=int,
+                   default=int(os.environ["EFL_BENCH_CPU_THREADS"]) if os.environ.get("EFL_BENCH_CPU_THREADS")
+                   else None, help="CPU baseline threads (default: every usable core)")
     p.add_argument("--tune", default=os.environ.get("EFL_FXP_TUNE", ""),
                    help="comma list kind=value for efl_fxp_tune (variant exploration)")
     p.add_argument("--rows", type=int, default=ROWS)
@@ -62,28 +93,20 @@ def parse():
     return p.parse_args()
 
 
-def setup_dist(args):
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    return world, rank, local
-
-
 def broadcast_seed(world, rank):
-    """RCCL broadcast of the key material (32-byte seed) from rank 0 over xGMI — the path's only
-    collective (efl.distributed.broadcast_key_material); timed apart from the steps."""
+    """Broadcast of the key material (32-byte seed) from rank 0 — the path's only collective
+    (efl.distributed.broadcast_key_material; RCCL over xGMI on an 8-GPU node); timed apart."""
     if world == 1:
         return os.urandom(32), 0.0
     from efl import distributed as edist
     seed, _ = edist.broadcast_key_material()          # warm the communicator
-    torch.cuda.synchronize()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(10):
         seed, _ = edist.broadcast_key_material(seed if rank == 0 else None)
-    torch.cuda.synchronize()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
     return seed, (time.perf_counter() - t0) / 10 * 1e6
 
 
@@ -97,21 +120,107 @@ def load_traffic():
         return None
 
 
-def cpu_baseline(x_dev, threads):
+def cpu_baseline(x_dev, threads, how, ftz):
+    """The reference op on the host: literal encode loop + GMP mpf decode, `threads` contiguous
+    blocks. The whole tensor takes about 0.1-0.3 s per pass on 16+ cores; median of 3."""
     from oracle import fxp
     x = x_dev.cpu().numpy().reshape(-1)
-    fxp.baseline_encode_decode(x[: 1 << 20], threads)          # warm
+    fxp.baseline_encode_decode(x[: 1 << 20], threads, ftz=ftz)          # warm
     times = []
     for _ in range(3):
         t0 = time.perf_counter()
-        fxp.baseline_encode_decode(x, threads)
+        fxp.baseline_encode_decode(x, threads, ftz=ftz)
         times.append(time.perf_counter() - t0)
     t = float(np.median(times))
     return {"value": round(x.nbytes / GIB / t, 4), "unit": "GiB/s", "cores": threads,
             "kind": "port",
-            "sample": f"whole 256 MiB tensor ({x.size} fp32), encode loop + GMP mpf decode "
-                      f"(fixed_point.cc:107-137, :235-248), {threads} threads, median of 3",
+            "sample": f"whole 256 MiB tensor ({x.size} fp32): the literal encode loop "
+                      f"(fixed_point.cc:107-137, float-convert ctz) + GMP mpf decode (:235-248) under "
+                      f"MXCSR {'FTZ|DAZ' if ftz else 'default'}, contiguous blocks like TF Shard on "
+                      f"{threads} threads ({how}), median of 3",
             "ms_per_step": round(t * 1e3, 2)}
+
+
+def config3(efl, dev, steps):
+    """BASELINE config 3: 4096 separate 64 KiB fp32 tensors ([128, 128] embedding slices,
+    N(0, 0.01), seed 1): one batched encode + one batched decode launch over device pointer
+    tables, against the naive 2 x 4096 per-slice launches."""
+    lib = efl.lib.raw()
+    slices, elems = 4096, 16384
+    g = torch.Generator(device=dev).manual_seed(1)
+    xs = [torch.randn(128, 128, device=dev, generator=g) * 0.01 for _ in range(slices)]
+    Ms = [torch.empty(128, 128, dtype=torch.int64, device=dev) for _ in range(slices)]
+    Es = [torch.empty(128, 128, dtype=torch.int64, device=dev) for _ in range(slices)]
+    ys = [torch.empty(128, 128, device=dev) for _ in range(slices)]
+    enc_t = efl.lib.BatchTables(xs, Ms, Es)
+    dec_t = efl.lib.BatchTables(Ms, Es, ys)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+    flags = 1 if efl.lib.flush_denormal() else 0
+
+    def batched():
+        efl.lib.encode_batched_into(enc_t, 1, False, sh)
+        efl.lib.decode_batched_into(dec_t, 1, flags, sh)
+
+    def naive():
+        for x, M, E in zip(xs, Ms, Es):
+            lib.efl_fxp_encode(x.data_ptr(), 1, M.data_ptr(), E.data_ptr(), elems, 0, sh)
+        for M, E, y in zip(Ms, Es, ys):
+            lib.efl_fxp_decode(M.data_ptr(), E.data_ptr(), y.data_ptr(), 1, elems, elems, flags, sh)
+
+    def wall(fn, k):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(k):
+            fn()
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) / k
+
+    t_b = wall(batched, max(10, steps))
+    ok = all(torch.equal(x, y) for x, y in zip(xs[::64], ys[::64]))
+    t_n = wall(naive, 3)
+    nbytes = slices * elems * 4
+    return {"workload": "config 3: 4096 x 64 KiB fp32 slices [128,128], batched encode+decode",
+            "GiBs": round(nbytes / GIB / t_b, 2), "ms": round(t_b * 1e3, 4),
+            "hbm_frac": round(2 * BYTES_PER_ELEM_KERNEL * slices * elems / t_b / 1e9 / PEAK_HBM_GBS, 4),
+            "naive_per_slice_ms": round(t_n * 1e3, 3), "naive_GiBs": round(nbytes / GIB / t_n, 3),
+            "launches": {"batched": 2, "naive": 2 * slices}, "roundtrip_ok": ok}
+
+
+def pinned_path(efl, dev, x_dev, reps=3):
+    """The north_star's rate including copies: the tensor starts and ends in pinned host memory
+    (the communicator's send/recv buffers). Encrypt leg: pinned fp32 -> H2D -> encode -> D2H ->
+    pinned M, E; decrypt leg: pinned M, E -> H2D -> decode -> D2H -> pinned fp32, each a chunked
+    pipeline over three streams (efl.framework.host_pipeline)."""
+    from efl.framework.host_pipeline import PinnedCodecPipeline
+    pipe = PinnedCodecPipeline(dev)
+    x = x_dev.reshape(-1).cpu().pin_memory()
+    n = x.numel()
+    M = torch.empty(n, dtype=torch.int64, pin_memory=True)
+    E = torch.empty(n, dtype=torch.int64, pin_memory=True)
+    y = torch.empty(n, dtype=torch.float32, pin_memory=True)
+    t_enc, t_dec = [], []
+    for r in range(reps + 1):
+        t0 = time.perf_counter()
+        pipe.encode(x, out=(M, E))
+        t1 = time.perf_counter()
+        pipe.decode(M, E, torch.float32, out=y)
+        t2 = time.perf_counter()
+        if r:
+            t_enc.append(t1 - t0)
+            t_dec.append(t2 - t1)
+    ok = bool(torch.equal(x.view(torch.int32), y.view(torch.int32)))
+    te, td = float(np.median(t_enc)), float(np.median(t_dec))
+    gib = n * 4 / GIB
+    return {"encrypt_GiBs": round(gib / te, 3), "decrypt_GiBs": round(gib / td, 3),
+            "encrypt_decrypt_GiBs": round(gib / (te + td), 3),
+            "encrypt_ms": round(te * 1e3, 2), "decrypt_ms": round(td * 1e3, 2),
+            "pcie_bytes_per_leg": {"encrypt": {"h2d": n * 4, "d2h": n * 16},
+                                   "decrypt": {"h2d": n * 16, "d2h": n * 4}},
+            "chunk_elems": pipe.chunk, "buffers": pipe.nbuf, "roundtrip_bit_exact": ok,
+            "how": "pinned host in/out, H2D | codec | D2H on three HIP streams, median of 3"}
 
 
 # ------------------------------------------------------------------------------------ Stage P
@@ -375,8 +484,11 @@ def stage_p_cpu(n_bytes, a_bytes, g, p, q, hs, threads, cache):
 def main():
     args = parse()
     if args.stage == "p":
+        if args.cpu_threads is None:
+            args.cpu_threads = usable_cores()[0]
         return stage_p(args)
-    world, rank, local = setup_dist(args)
+    from efl import distributed as edist
+    world, rank, local, dev_index, backend = edist.init_from_env(args.backend)
     import efl
     dev = efl.lib.require_gpu()
     lib = efl.lib.raw()
@@ -393,50 +505,58 @@ def main():
     y = torch.empty_like(x)
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
+    ftz = efl.lib.flush_denormal()
+    flags = 1 if ftz else 0
+    xp, Mp, Ep, yp = x.data_ptr(), M.data_ptr(), E.data_ptr(), y.data_ptr()
+    enc, dec = lib.efl_fxp_encode, lib.efl_fxp_decode
 
-    def step(ev0=None, ev1=None, ev2=None):
-        if ev0 is not None:
-            ev0.record(stream)
-        efl.lib.check(lib.efl_fxp_encode(x.data_ptr(), 1, M.data_ptr(), E.data_ptr(), n, 0, sh))
-        if ev1 is not None:
-            ev1.record(stream)
-        efl.lib.check(lib.efl_fxp_decode(M.data_ptr(), E.data_ptr(), y.data_ptr(), 1, n, n, 0, sh))
-        if ev2 is not None:
-            ev2.record(stream)
+    def step():
+        rc = enc(xp, 1, Mp, Ep, n, 0, sh) or dec(Mp, Ep, yp, 1, n, n, flags, sh)
+        if rc:
+            efl.lib.check(rc)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    # correctness gate before timing: round trip must be the identity on non-zero values
-    nz = x != 0
-    if not torch.equal(y[nz], x[nz]):
+    # correctness gate before timing: with FTZ the round trip is the identity on every bit
+    # pattern torch.randn makes (no denormals; +-0.0 -> +-0.0)
+    if not torch.equal(y.view(torch.int32), x.view(torch.int32)) if ftz else \
+            not torch.equal(y[x != 0], x[x != 0]):
         raise SystemExit("bench: encode/decode round trip is wrong")
 
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    # ---- timed region: K steps, nothing else -------------------------------------------------
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(*evs[k])
+    for _ in range(args.steps):
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+
+    # ---- per-kernel durations: a second pass of K steps with HIP events on the launch stream -
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    for k in range(args.steps):
+        evs[k][0].record(stream)
+        efl.lib.check(enc(xp, 1, Mp, Ep, n, 0, sh))
+        evs[k][1].record(stream)
+        efl.lib.check(dec(Mp, Ep, yp, 1, n, n, flags, sh))
+        evs[k][2].record(stream)
+    torch.cuda.synchronize()
     t_enc = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))   # ms
     t_dec = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
     if world > 1:
-        tt = torch.tensor([elapsed, t_enc, t_dec], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed, t_enc, t_dec = tt.tolist()
+        elapsed, t_enc, t_dec = edist.all_reduce_max([elapsed, t_enc, t_dec])
 
     ms_per_step = elapsed / args.steps * 1e3
     value = world * (n * 4) / GIB / (elapsed / args.steps)
 
     # practical peak: device-to-device copy of the same byte volume as one kernel
-    buf_a = torch.empty(n * 5 // 4, dtype=torch.float64, device=dev) if rank == 0 else None
     copy_gbs = None
     if rank == 0:
+        buf_a = torch.empty(n * 5 // 4, dtype=torch.float64, device=dev)
         buf_b = torch.empty_like(buf_a)
         for _ in range(3):
             buf_b.copy_(buf_a)
@@ -476,21 +596,30 @@ def main():
         "data": "synthetic: torch.randn fp32 on device, generator seed = rank",
         "config": {"workload": "config 2: single 256 MiB fp32 tensor [65536,1024] per GPU, "
                                "device-resident ConvertToFixedPoint + FixedPointToFloatPoint",
-                   "elements_per_gpu": n, "decrease_precision": False,
-                   "parallelism": f"element-wise shard, {world} x 256 MiB, RCCL seed broadcast"},
+                   "elements_per_gpu": n, "decrease_precision": False, "decode_ftz": ftz,
+                   "parallelism": f"element-wise shard, {world} x 256 MiB, {backend if world > 1 else 'no'} "
+                                  f"seed broadcast"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
                      "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
                      "traffic": traffic, "kernel": dominant,
-                     "algorithmic_bytes_per_launch": BYTES_PER_ELEM_KERNEL * n},
+                     "algorithmic_bytes_per_launch": BYTES_PER_ELEM_KERNEL * n,
+                     "timing": "HIP events around each launch, second pass of K steps after the timed region"},
         "kernels_ms": {"encode": round(t_enc, 4), "decode": round(t_dec, 4)},
-        "step_roofline_frac": round(2 * BYTES_PER_ELEM_KERNEL * n / ((t_enc + t_dec) * 1e-3) / 1e9
-                                    / PEAK_HBM_GBS, 4),
+        "step_roofline_frac": round(2 * BYTES_PER_ELEM_KERNEL * n / (ms_per_step * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
         "d2d_copy_GBs": round(copy_gbs, 1) if copy_gbs else None,
         "seed_broadcast_us": round(bcast_us, 2),
+        "backend": backend if world > 1 else None,
+        "devices_used": torch.cuda.device_count() if world == 1 else min(world, torch.cuda.device_count()),
+        "library": efl.lib.version(),
         "cpu_baseline": None,
     }
+    if world == 1 and not args.no_extras:
+        del M, E, y
+        out["config3"] = config3(efl, dev, args.steps)
+        out["pinned_path"] = pinned_path(efl, dev, x)
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(x, args.cpu_threads)
+        threads, how = (args.cpu_threads, "--cpu-threads") if args.cpu_threads else usable_cores()
+        out["cpu_baseline"] = cpu_baseline(x, threads, how, ftz)
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -130,7 +130,11 @@ __device__ __forceinline__ void st(T* p, T v) {
     const i4 w = __builtin_bit_cast(i4, v);
     // The compiler's hazard recognizer does not see a store inside inline asm: a VALU write to
     // the data VGPRs right after a >8-byte store needs a wait state on gfx950, so pad it here.
+    // tests/test_isa_guard.py checks every such store in the built library keeps its s_nop.
     asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" ::"v"(p), "v"(w) : "memory");
+  } else if constexpr ((NT & 4) && sizeof(T) == 8) {
+    const i2 w = __builtin_bit_cast(i2, v);
+    asm volatile("global_store_dwordx2 %0, %1, off nt sc1\n\ts_nop 1" ::"v"(p), "v"(w) : "memory");
   } else if constexpr (NT & 2) {
     __builtin_nontemporal_store(v, p);
   } else {
@@ -433,17 +437,19 @@ __global__ __launch_bounds__(kBlock) void k_decode_hex(const char* chars, const 
 
 // Per-direction launch shape of the fp32 kernels. Defaults: the fastest shape of the interleaved
 // sweep on MI355X (tools/sweep_fxp.py -> profiles/r01/sweep_*.jsonl), pair layout, one tile per
-// workgroup. Decode: 128 lanes, nontemporal loads (+5 % over plain loads). Encode: 256 lanes,
-// nontemporal loads and `nt sc1` stores (NT mask 7): in the bench step 0.197 vs 0.209 ms for
-// 128 lanes / plain stores, and 1.5-3 % below plain `nt` stores (profiles/r01/ab_*.json,
-// tools/enc_probe.hip on the bare mix); it also takes decode's time down (no inherited dirty lines).
+// workgroup. Decode: 128 lanes, nontemporal loads (+5 % over plain loads; plain stores: `nt sc1`
+// stores cost 4 % of the step, profiles/r02/step_probe_*.json). Encode: 512 lanes, nontemporal
+// loads and `nt sc1` stores (NT mask 7): 256 lanes took the bench step from 0.209 to 0.197 ms over
+// 128 lanes / plain stores, and 512 lanes another 1-2 % (step_probe, two boxes); `nt sc1` is
+// 1.5-3 % below plain `nt` stores (profiles/r01/ab_*.json, tools/enc_probe.hip on the bare mix)
+// and also takes decode's time down (no inherited dirty lines).
 struct Shape {
   std::atomic<int> variant;   // 0 pair, 1 quad
-  std::atomic<int> block;     // 128, 256, 512
+  std::atomic<int> block;     // 128, 256, 512, 1024
   std::atomic<int> k;         // units per lane per tile: 1, 2
   std::atomic<int> nt;        // bit0 nontemporal loads, bit1 nontemporal stores
 };
-Shape g_shape[2] = {{{0}, {256}, {1}, {7}}, {{0}, {128}, {1}, {1}}};
+Shape g_shape[2] = {{{0}, {512}, {1}, {7}}, {{0}, {128}, {1}, {1}}};
 std::atomic<int> g_grid_cap{0};   // 0: one tile per workgroup; else max workgroups
 // NT mask of the fp32 batched encode (efl_fxp_tune kind 9): 1 nontemporal loads, 3 loads + stores,
 // 7 loads + `nt sc1` stores (default, as the streaming encode)
@@ -486,6 +492,7 @@ hipError_t launch_tuned(const Shape& sh, const typename Op::Args& a, long long n
   switch (sh.block.load(std::memory_order_relaxed)) {
     case 128: return launch_bk<Op, 128>(sh, a, nunits, s);
     case 512: return launch_bk<Op, 512>(sh, a, nunits, s);
+    case 1024: return launch_bk<Op, 1024>(sh, a, nunits, s);
     default: return launch_bk<Op, 256>(sh, a, nunits, s);
   }
 }
@@ -550,8 +557,6 @@ int hip_status(hipError_t e, const char* what) {
 
 using namespace efl;
 
-EFL_API const char* efl_version(void) { return "efl-hip 0.1.0 (gfx950)"; }
-
 EFL_API const char* efl_last_error(void) { return t_err.c_str(); }
 
 EFL_API int efl_fxp_tune(int kind, int value) {
@@ -576,7 +581,7 @@ EFL_API int efl_fxp_tune(int kind, int value) {
       if (value < 0 || (value > 3 && value != 7)) return EFL_E_INVALID_ARGUMENT;
       return sh.nt.exchange(value);
     default:
-      if (value != 128 && value != 256 && value != 512) return EFL_E_INVALID_ARGUMENT;
+      if (value != 128 && value != 256 && value != 512 && value != 1024) return EFL_E_INVALID_ARGUMENT;
       return sh.block.exchange(value);
   }
 }

@@ -4,10 +4,11 @@ The path is element-wise: a tensor is cut into contiguous, 25
 element ranges, one per rank, and every rank transforms its range with no payload exchange. The
 only collective is a broadcast from rank 0 of the key material every rank needs — the 32-byte seed
 of the per-element randomness counter stream and, once a Paillier key exists, the public key —
-RCCL over xGMI on MI355X (`nccl` backend), gloo on CPU.
+RCCL over xGMI on MI355X (`nccl` backend), gloo when ranks share one GPU or run on CPU.
 
 Each rank's counter base is the global element offset of its range, so results do not depend on
-the number of GPUs (tests/test_distributed.py checks that invariant).
+the number of GPUs (tests/test_distributed.py and tests/test_distributed_gpu.py check that
+invariant, the latter with the HIP kernels under two ranks).
 """
 from __future__ import annotations
 
@@ -34,11 +35,47 @@ def shard_range(n: int, world: int, rank: int, elem_bytes: int = 4):
     return min(n, s_units * quantum), min(n, e_units * quantum)
 
 
+def choose_backend(world: int, backend: str | None = None) -> str:
+    """RCCL (`nccl`) when every rank has a GPU of its own; gloo when ranks must share a device
+    (RCCL refuses two ranks on one GPU) or there is no GPU."""
+    if backend:
+        return backend
+    ndev = torch.cuda.device_count()          # does not initialise the GPU on this image
+    return "nccl" if ndev >= max(1, world) else "gloo"
+
+
+def init_from_env(backend: str | None = None):
+    """Join the process group torchrun describes (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*).
+    Returns (world, rank, local_rank, device index or None, backend)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    dev_index = (local % ndev) if ndev else None
+    be = choose_backend(world, backend)
+    if world > 1:
+        if be == "nccl":
+            torch.cuda.set_device(dev_index)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            if dev_index is not None:
+                torch.cuda.set_device(dev_index)
+            dist.init_process_group("gloo")
+    return world, rank, local, dev_index, be
+
+
 def _device_for(group=None):
     backend = dist.get_backend(group)
     if backend == "nccl":
         return torch.device("cuda", torch.cuda.current_device())
     return torch.device("cpu")
+
+
+def all_reduce_max(values, group=None):
+    """Element-wise max over ranks of a list of floats (on the backend's device)."""
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=_device_for(group))
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return t.tolist()
 
 
 def broadcast_key_material(seed: bytes | None = None, public_key: dict | None = None, src: int = 0,
@@ -61,3 +98,22 @@ def broadcast_key_material(seed: bytes | None = None, public_key: dict | None = 
     dist.broadcast(buf, src, group=group)
     msg = json.loads(bytes(buf.cpu().numpy()).decode())
     return bytes.fromhex(msg["seed"]), msg["public_key"]
+
+
+def shard_keypair(seed: bytes, public_key: dict, n: int, world: int, rank: int, private_key=None):
+    """The Paillier keypair one rank encrypts its shard of an n-element tensor with: the broadcast
+    public key {n, hs, a_bytes, group_size[, n_bytes]} (hex ints), randomness keyed by the
+    broadcast seed, and the running counter started at the shard's global element offset, so
+    rank r's ciphertexts equal elements [start, end) of a single-GPU encryption under the same
+    seed (Philox counter = global element index). Returns (keypair, (start, end))."""
+    from efl.privacy.paillier_cipher import PaillierKeypair
+    start, end = shard_range(n, world, rank, elem_bytes=8)
+    kp = PaillierKeypair(seed=seed)
+    pk = public_key
+    p = q = None
+    if private_key is not None:
+        p, q = int(private_key["p"], 16), int(private_key["q"], 16)
+    kp.set_keys_ints(int(pk["n"], 16), int(pk["hs"], 16), int(pk["a_bytes"]), int(pk.get("group_size", 1)),
+                     p, q, pk.get("n_bytes"))
+    kp.counter = start
+    return kp, (start, end)

@@ -56,7 +56,13 @@ _TORCH_TO_DT = {torch.float32: DT_FLOAT, torch.float64: DT_DOUBLE, torch.int32: 
                 torch.int16: DT_INT16, torch.int8: DT_INT8, torch.int64: DT_INT64}
 _DT_TO_TORCH = {v: k for k, v in _TORCH_TO_DT.items()}
 
-_flush_denormal = False
+# Decode's float32 rounding mode. The reference op's kernels run on TensorFlow threadpool threads,
+# and TF 1.15 starts every threadpool thread with MXCSR FTZ|DAZ set (tensorflow/core/platform/
+# threadpool.cc, EigenEnvironment::CreateThread: port::ScopedFlushDenormal; TF 1.15.5 is the
+# reference's base image, docker/Dockerfile.efls-train:1). The implicit double -> float of
+# fixed_point.cc:245 therefore flushes results below 2^-126 to signed zero: +-0.0 (encoded as
+# (+-1, -127)) decodes to +-0.0, not 2^-127. That is the default here.
+_flush_denormal = True
 
 
 def raw():
@@ -70,8 +76,8 @@ def version() -> str:
 
 def set_flush_denormal(enabled: bool) -> bool:
     """Decode float32 results below the normal range to signed zero, as the reference does inside
-    TensorFlow's threadpool threads (MXCSR FTZ|DAZ). Default False = the bare reference loop
-    (SURVEY.md Appendix A). Returns the previous setting."""
+    TensorFlow's threadpool threads (MXCSR FTZ|DAZ). Default True; False reproduces the bare loop
+    compiled outside TF (+0.0 -> 2^-127). Returns the previous setting."""
     global _flush_denormal
     old, _flush_denormal = _flush_denormal, bool(enabled)
     return old
@@ -286,14 +292,34 @@ def decode_batched_into(tables: BatchTables, dtype_code: int, flags=0, stream=No
                                       stream if stream is not None else stream_handle()))
 
 
-def fixed_point_to_float_point_batched(mantissas, exponents, dtype=torch.float32):
+def fixed_point_to_float_point_batched(mantissas, exponents, dtype=torch.float32, flush_denormal=None):
+    """One launch decoding a list of (mantissa, exponent) int64 device tensor pairs. Each pair is
+    checked like efl_fxp_decode checks one (same size, fixed_point.cc:230-232) and made contiguous
+    first, so a strided view is decoded from its own elements."""
+    if len(mantissas) != len(exponents):
+        raise errors.InvalidArgumentError("batched decode: as many exponents as mantissas")
     if not mantissas:
         return []
     dtype = to_torch_dtype(dtype)
+    if dtype not in (torch.float32, torch.float64):
+        raise errors.InvalidArgumentError(f"FixedPointToFloatPoint: dtype must be float or double, got {dtype}")
     dev = mantissas[0].device
-    ys = [torch.empty(m.shape, dtype=dtype, device=dev) for m in mantissas]
-    tables = BatchTables(mantissas, exponents, ys)
-    decode_batched_into(tables, dt_code(dtype), 1 if _flush_denormal else 0, stream_handle(dev))
+    if dev.type != "cuda":
+        raise errors.InvalidArgumentError("batched ops take device tensors")
+    ms, es = [], []
+    for i, (m, e) in enumerate(zip(mantissas, exponents)):
+        if m.dtype != torch.int64 or e.dtype != torch.int64:
+            raise errors.InvalidArgumentError(f"batched decode: pair {i}: mantissa and exponent must be int64")
+        if m.device != dev or e.device != dev:
+            raise errors.InvalidArgumentError(f"batched decode: pair {i} is not on {dev}")
+        if m.numel() != e.numel():
+            raise errors.InvalidArgumentError(f"batched decode: pair {i}: mantissa and exponent should be the same size.")
+        ms.append(m.contiguous())
+        es.append(e.contiguous())
+    ftz = _flush_denormal if flush_denormal is None else bool(flush_denormal)
+    ys = [torch.empty(m.shape, dtype=dtype, device=dev) for m in ms]
+    tables = BatchTables(ms, es, ys)
+    decode_batched_into(tables, dt_code(dtype), 1 if ftz else 0, stream_handle(dev))
     return ys
 
 

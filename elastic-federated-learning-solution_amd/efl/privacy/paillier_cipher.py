@@ -15,6 +15,7 @@ handed to string-typed callers.
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import math
 import os
 import secrets
@@ -449,6 +450,19 @@ def _is_string_dtype(dtype) -> bool:
     return dtype in ("string", str, bytes, "str") or getattr(dtype, "name", None) == "string"
 
 
+def philox_key(seed: bytes | int | None = None) -> int:
+    """64-bit Philox4x32-10 key of a keypair's randomness stream. Bytes (the 32-byte seed rank 0
+    broadcasts, efl.distributed) are hashed whole (BLAKE2b-64), so every seed byte matters; an int
+    is taken mod 2^64; None draws from os.urandom. Philox is a counter-based generator, not a
+    cryptographic PRF; it replaces the reference's time()-seeded MT19937 (paillier.cc:54-57), which
+    is weaker still (Randomness)."""
+    if seed is None:
+        seed = os.urandom(32)
+    if isinstance(seed, (bytes, bytearray)):
+        return int.from_bytes(hashlib.blake2b(bytes(seed), digest_size=8).digest(), "little")
+    return int(seed) & ((1 << 64) - 1)
+
+
 @exporter.export("paillier.Keypair")
 class PaillierKeypair(object):
     """paillier.py:53-104 over the PaillierKeypair resource (paillier.cc:50-331)."""
@@ -456,11 +470,7 @@ class PaillierKeypair(object):
     def __init__(self, seed: bytes | int | None = None):
         self._key: KeyBlock | None = None
         self._n_bytes = None
-        if seed is None:
-            seed = os.urandom(8)
-        if isinstance(seed, (bytes, bytearray)):
-            seed = int.from_bytes(bytes(seed)[:8].ljust(8, b"\0"), "little")
-        self.seed = int(seed) & ((1 << 64) - 1)
+        self.seed = philox_key(seed)
         self.counter = 0
 
     # -- key management ------------------------------------------------------------------
@@ -543,6 +553,9 @@ class PaillierKeypair(object):
             if not strs_zero.all():
                 hsa_limbs, _ = hex_to_limbs(hx, k.lc, k.device)
             zero_idx = np.nonzero(strs_zero)[0] if hsa_limbs is not None else None
+        # element i draws its a from Philox counter ctr + i: the call owns [ctr, ctr + N) and the
+        # running counter moves past it, so no two elements of any two calls share an a (a shared
+        # a gives equal hs^a factors, and the quotient of the two ciphertexts reveals m1 - m2)
         ctr = self.counter if counter_base is None else int(counter_base)
         if counter_base is None:
             self.counter += N
@@ -550,17 +563,28 @@ class PaillierKeypair(object):
                                            hsa_limbs.data_ptr() if hsa_limbs is not None else None,
                                            out.data_ptr(), N, self.seed, ctr, _stream(k.device)))
         if hsa_limbs is not None and zero_idx is not None and zero_idx.size:
+            # the rows whose hsa is "0" draw a fresh a at their own index's counter (ctr + idx),
+            # inside this call's range: rows with a given hsa consume no counter
             idx = torch.from_numpy(zero_idx).to(k.device)
             sub = torch.empty((idx.numel(), k.lc), dtype=torch.int32, device=k.device)
             msub = m[idx].contiguous()
-            _efl_lib.check(_lib.efl_pl_encrypt(*k.args(), msub.data_ptr(), None, sub.data_ptr(), idx.numel(),
-                                               self.seed, ctr + N, _stream(k.device)))
+            for j0, j1, c0 in _counter_runs(zero_idx):
+                _efl_lib.check(_lib.efl_pl_encrypt(*k.args(), msub[j0:j1].data_ptr(), None, sub[j0:j1].data_ptr(),
+                                                   j1 - j0, self.seed, ctr + c0, _stream(k.device)))
             out[idx] = sub
         return PaillierTensor(self, CipherTensor(out, shape, k))
 
-    def fbpowm(self, a=None, n=None, counter_base=0):
-        """hs^(a') mod n^2 for given exponents (Python ints) or the Philox draw (FixedBasePowm)."""
+    def fbpowm(self, a=None, n=None, counter_base=None):
+        """hs^(a') mod n^2 for given exponents (Python ints) or the Philox draw (FixedBasePowm).
+        A Philox draw takes its counters from the running counter (like encrypt) unless
+        counter_base is given, so it never repeats an a an encryption used."""
         k = self.key
+        if a is None:
+            if counter_base is None:
+                counter_base = self.counter
+                self.counter += int(n)
+        else:
+            counter_base = 0
         words = (k.a_bits + 31) // 32
         if a is not None:
             a = list(a)
@@ -684,6 +708,18 @@ class PaillierKeypair(object):
         if any(y < 0 for y in ys):
             raise errors.InvalidArgumentError("y should be a positive tensor.")
         return self._powm(x, [1 << y for y in ys])
+
+
+def _counter_runs(idx: np.ndarray):
+    """Sorted element indices -> (j0, j1, first index) runs of consecutive indices, so each run
+    is one launch whose element t draws counter (first index + t)."""
+    runs = []
+    j0 = 0
+    for j in range(1, idx.size + 1):
+        if j == idx.size or idx[j] != idx[j - 1] + 1:
+            runs.append((j0, j, int(idx[j0])))
+            j0 = j
+    return runs
 
 
 def _scalar_list(s, shape):

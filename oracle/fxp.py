@@ -9,6 +9,9 @@ Two independent CPU restatements of efls-train's fixed-point codec
             each other (tests/test_oracle.py).
 
 Rules follow SURVEY.md Appendix A (A1-A6) for encode and GMP mpf_get_d truncation for decode.
+Decode defaults to the MXCSR FTZ|DAZ state the reference op runs in inside TensorFlow (its kernels
+execute on TF threadpool threads, which set flush-to-zero); ftz=False gives the bare
+loop's output (+0.0 -> 2^-127).
 """
 from __future__ import annotations
 
@@ -49,7 +52,8 @@ def lib():
         L.gmp_decode_hex.argtypes = [vp, vp, vp, vp, i32, i64, i32]
         L.gmp_decode_hex.restype = i64
         L.baseline_encode_f32_mt.argtypes = [vp, vp, vp, i64, i32, i32]
-        L.baseline_decode_f32_mt.argtypes = [vp, vp, vp, i64, i32]
+        L.baseline_decode_f32_mt.argtypes = [vp, vp, vp, i64, i32, i32]
+        L.baseline_encode_f32_literal.argtypes = [vp, vp, vp, i64, i32]
         _lib = L
     return _lib
 
@@ -78,8 +82,9 @@ def encode(x: np.ndarray, decrease_precision: bool = False):
     return M, E
 
 
-def decode(M: np.ndarray, E: np.ndarray, dtype=np.float32, ftz: bool = False):
-    """FixedPointToFloatPoint<int64, dtype> (fixed_point.cc:201-287)."""
+def decode(M: np.ndarray, E: np.ndarray, dtype=np.float32, ftz: bool = True):
+    """FixedPointToFloatPoint<int64, dtype> (fixed_point.cc:201-287). ftz (default, as the op runs
+    on a TF threadpool thread): float results below the normal range flush to signed zero."""
     M = np.ascontiguousarray(M, np.int64)
     E = np.ascontiguousarray(E, np.int64)
     if M.size != E.size:
@@ -102,7 +107,7 @@ def pack_hex(strings):
     return buf, offs
 
 
-def decode_hex(strings, E: np.ndarray, dtype=np.float32, ftz: bool = False):
+def decode_hex(strings, E: np.ndarray, dtype=np.float32, ftz: bool = True):
     """FixedPointToFloatPoint<string, dtype> restated (top-64-bit truncation)."""
     E = np.ascontiguousarray(E, np.int64).reshape(-1)
     out = np.empty(E.shape, np.float64 if np.dtype(dtype) == np.float64 else np.float32)
@@ -120,7 +125,7 @@ def decode_hex(strings, E: np.ndarray, dtype=np.float32, ftz: bool = False):
 
 # ------------------------------------------------------------------------------ GMP pin
 
-def gmp_decode(M, E, dtype=np.float32, ftz=False):
+def gmp_decode(M, E, dtype=np.float32, ftz=True):
     """Decode through GMP 6.2.1 mpf in the reference's call order (pinning only)."""
     M = np.ascontiguousarray(M, np.int64)
     E = np.ascontiguousarray(E, np.int64)
@@ -130,7 +135,7 @@ def gmp_decode(M, E, dtype=np.float32, ftz=False):
     return y
 
 
-def gmp_decode_hex(strings, E, dtype=np.float32, ftz=False):
+def gmp_decode_hex(strings, E, dtype=np.float32, ftz=True):
     buf, offs = pack_hex(strings)
     E = np.ascontiguousarray(E, np.int64)
     f64 = np.dtype(dtype) == np.float64
@@ -141,16 +146,26 @@ def gmp_decode_hex(strings, E, dtype=np.float32, ftz=False):
 
 # ------------------------------------------------------------------------ CPU baseline
 
-def baseline_encode_decode(x: np.ndarray, nthreads: int, decrease_precision=False):
-    """Reference op timing stand-in: encode loop + GMP-mpf decode loop, sharded over threads."""
+def baseline_encode_decode(x: np.ndarray, nthreads: int, decrease_precision=False, ftz=True):
+    """Reference op timing stand-in: the literal encode loop + GMP-mpf decode loop, sharded over
+    threads (decode under MXCSR FTZ|DAZ when ftz, as on a TF threadpool thread)."""
     x = np.ascontiguousarray(x, np.float32)
     n = x.size
     M = np.empty(n, np.int64)
     E = np.empty(n, np.int64)
     y = np.empty(n, np.float32)
     lib().baseline_encode_f32_mt(_p(x), _p(M), _p(E), n, int(bool(decrease_precision)), nthreads)
-    lib().baseline_decode_f32_mt(_p(M), _p(E), _p(y), n, nthreads)
+    lib().baseline_decode_f32_mt(_p(M), _p(E), _p(y), n, nthreads, int(bool(ftz)))
     return M, E, y
+
+
+def literal_encode_f32(x: np.ndarray, decrease_precision=False):
+    """The reference loop body statement for statement (float-convert ctz), one thread."""
+    x = np.ascontiguousarray(x, np.float32)
+    M = np.empty(x.shape, np.int64)
+    E = np.empty(x.shape, np.int64)
+    lib().baseline_encode_f32_literal(_p(x), _p(M), _p(E), x.size, int(bool(decrease_precision)))
+    return M, E
 
 
 # ----------------------------------------------------------------- numpy restatement
@@ -224,7 +239,7 @@ def np_get_d_bits(M: np.ndarray, E: np.ndarray) -> np.ndarray:
     return bits
 
 
-def np_decode_f32(M, E, ftz=False):
+def np_decode_f32(M, E, ftz=True):
     d = np_get_d_bits(M, E).view(np.float64)
     with np.errstate(over="ignore"):
         f = d.astype(np.float32)

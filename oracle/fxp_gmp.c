@@ -105,6 +105,43 @@ EFL_EXPORT int64_t gmp_decode_hex(const char* buf, const int64_t* offs, const in
 
 /* ---------------------------- threaded CPU baseline ---------------------------------- */
 
+/* The reference's encode loop body as it runs (fixed_point.cc:107-137), statement for statement,
+ * for the timed baseline: the trailing-zero count is taken the reference's way, by converting the
+ * lowest set bit to float and reading its biased exponent (:126-127), not with a ctz instruction.
+ * The mant == 0 case shifts by (0u - 127) like the reference; gcc on x86-64 gives M = 0,
+ * E = exp - 127 there, which tests/test_oracle.py checks against the
+ * restatement in fxp_oracle.c. */
+static void encode_f32_literal(const float* x, int64_t* M, int64_t* E, int64_t s, int64_t e,
+                               int dp) {
+  for (int64_t i = s; i < e; ++i) {
+    uint32_t bits;
+    memcpy(&bits, &x[i], sizeof bits);
+    uint32_t se = bits >> 23;
+    uint32_t sign = se >> 8;
+    int exp = (int)(se & 0xFFu) - 127 - 23;
+    int mant = (int)(bits & 0x7FFFFFu);
+    if (exp) mant |= 0x800000;
+    if (dp) {
+      mant >>= 13;
+      exp += 13;
+    }
+    float low = (float)(mant & -mant);
+    uint32_t lbits;
+    memcpy(&lbits, &low, sizeof lbits);
+    unsigned r = (lbits >> 23) - 127u;
+    mant = (int)((unsigned)mant >> (r & 31u));
+    exp = (int)((unsigned)exp + r);
+    M[i] = sign ? -(int64_t)mant : (int64_t)mant;
+    E[i] = exp;
+  }
+}
+
+/* Single-threaded literal loop (checked against the restatement by tests/test_oracle.py). */
+EFL_EXPORT void baseline_encode_f32_literal(const float* x, int64_t* M, int64_t* E, int64_t n,
+                                            int dp) {
+  encode_f32_literal(x, M, E, 0, n, dp);
+}
+
 typedef struct {
   const void* x;
   const int64_t* Mi;
@@ -121,7 +158,7 @@ static void* worker(void* p) {
   job_t* j = (job_t*)p;
   unsigned old = set_ftz(j->ftz);
   if (j->mode == 0) {
-    oracle_encode_f32((const float*)j->x + j->s, j->M + j->s, j->E + j->s, j->e - j->s, j->dp);
+    encode_f32_literal((const float*)j->x, j->M, j->E, j->s, j->e, j->dp);
   } else {
     decode_i64_range(j->Mi, j->Ei, j->y, 0, j->s, j->e);
   }
@@ -145,7 +182,8 @@ static void run_sharded(job_t proto, int64_t n, int nthreads) {
   free(jobs);
 }
 
-/* Reference encode loop (fixed_point.cc:107-137) sharded over nthreads contiguous blocks. */
+/* Reference encode loop (fixed_point.cc:107-137, literal form above) sharded over nthreads
+ * contiguous blocks like TF Shard (:140-141). */
 EFL_EXPORT void baseline_encode_f32_mt(const float* x, int64_t* M, int64_t* E, int64_t n, int dp,
                                        int nthreads) {
   job_t j;
@@ -154,11 +192,12 @@ EFL_EXPORT void baseline_encode_f32_mt(const float* x, int64_t* M, int64_t* E, i
   run_sharded(j, n, nthreads);
 }
 
-/* Reference decode loop (fixed_point.cc:235-248, GMP mpf) sharded over nthreads blocks. */
+/* Reference decode loop (fixed_point.cc:235-248, GMP mpf) sharded over nthreads blocks; ftz = the
+ * MXCSR state of a TF threadpool thread (FTZ|DAZ), the mode the GPU leg decodes in. */
 EFL_EXPORT void baseline_decode_f32_mt(const int64_t* M, const int64_t* E, float* y, int64_t n,
-                                       int nthreads) {
+                                       int nthreads, int ftz) {
   job_t j;
   memset(&j, 0, sizeof(j));
-  j.Mi = M; j.Ei = E; j.y = y; j.mode = 1; j.ftz = 1;
+  j.Mi = M; j.Ei = E; j.y = y; j.mode = 1; j.ftz = ftz;
   run_sharded(j, n, nthreads);
 }

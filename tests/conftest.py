@@ -15,7 +15,9 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libefl_hip.so)")
-    # build the oracle (CPU checker) and the HIP library if they are missing
+    # build the oracle (CPU checker) and the HIP library if they are missing; an existing library
+    # is never rebuilt here (tests/test_abi.py::test_library_built_from_this_tree fails if it is
+    # stale), so a GPU run uses exactly the .so that was pushed with the tree
     if not os.path.exists(os.path.join(ROOT, "oracle", "build", "liboracle.so")):
         subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
     if not os.path.exists(os.path.join(PKG, "efl", "libefl_hip.so")):

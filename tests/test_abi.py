@@ -57,6 +57,30 @@ def test_pl_key_struct_matches_ctypes_mirror(tmp_path):
     assert got[1:] == [getattr(PlKey, n).offset for n in names]
 
 
+def source_hash():
+    """The hash the Makefile embeds into efl_version(): sha256 of csrc/*.hip, *.h, *.cpp in sorted
+    path order, then include/efl_hip.h (elastic-federated-learning-solution_amd/Makefile)."""
+    import glob
+    import hashlib
+    csrc = os.path.join(PKG, "csrc")
+    files = sorted(os.path.relpath(p, PKG) for pat in ("*.hip", "*.h", "*.cpp")
+                   for p in glob.glob(os.path.join(csrc, pat)))
+    h = hashlib.sha256()
+    for f in files:
+        h.update(open(os.path.join(PKG, f), "rb").read())
+    h.update(open(os.path.join(ROOT, "include", "efl_hip.h"), "rb").read())
+    return h.hexdigest()[:16]
+
+
+def test_library_built_from_this_tree():
+    """efl_version() names the sources the .so was built from; a stale library (sources edited,
+    not rebuilt) fails here instead of silently running old kernels."""
+    lib = ctypes.CDLL(LIB)
+    lib.efl_version.restype = ctypes.c_char_p
+    v = lib.efl_version().decode()
+    assert v.endswith("src " + source_hash()), (v, source_hash())
+
+
 def test_library_is_gfx950_code_object():
     blob = open(LIB, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob

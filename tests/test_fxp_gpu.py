@@ -127,6 +127,52 @@ def test_decode_hex_malformed(efl):
         efl.lib.ops.fixed_point_to_float_point(hx, dev(np.zeros(3, np.int64)))
 
 
+@pytest.mark.parametrize("ftz", [None, 0, 1])
+def test_relu_zeros_and_denormals_both_modes(efl, ftz):
+    """ReLU-style activations (half exact zeros), +-0.0 and every denormal class,
+    round-tripped through the GPU codec and compared with GMP run in the same MXCSR mode. The
+    default (ftz=None) is the op as TF runs it (FTZ|DAZ): zeros come back as signed zeros."""
+    rng = np.random.default_rng(21)
+    x = np.maximum(rng.standard_normal(1 << 16).astype(np.float32), 0)     # ReLU
+    x[:8] = np.array([0.0, -0.0, 1e-45, -1e-45, 1e-40, -1e-39, 1.1754942e-38, -1.1754942e-38], np.float32)
+    x[8:40] = (np.arange(1, 33, dtype=np.uint32) << np.uint32(18)).view(np.float32)   # denormals
+    fp = efl.paillier.fixedpoint.encode(dev(x))
+    Mo, Eo = fxp.encode(x)
+    assert np.array_equal(host(fp.mantissa), Mo) and np.array_equal(host(fp.exponent), Eo)
+    mode = True if ftz is None else bool(ftz)
+    y = efl.lib.ops.fixed_point_to_float_point(fp.mantissa, fp.exponent, flush_denormal=None if ftz is None else mode)
+    want = fxp.gmp_decode(Mo, Eo, np.float32, mode).view(np.uint32)
+    assert np.array_equal(bits32(y), want)
+    if mode:      # FTZ: zeros keep their sign, denormal inputs flush to signed zero
+        assert bits32(y)[0] == 0 and bits32(y)[1] == 0x80000000
+        assert (bits32(y)[(x == 0)] & 0x7FFFFFFF == 0).all()
+        normal = np.abs(x) >= np.float32(1.1754944e-38)
+        assert np.array_equal(bits32(y)[normal], x[normal].view(np.uint32))
+    else:         # bare loop: +-0.0 -> +-2^-127
+        assert bits32(y)[0] == 0x00400000 and bits32(y)[1] == 0x80400000
+    # the batched decode honours the same mode
+    ys = efl.lib.ops.fixed_point_to_float_point_batched([fp.mantissa[:1000], fp.mantissa],
+                                                        [fp.exponent[:1000], fp.exponent],
+                                                        flush_denormal=None if ftz is None else mode)
+    assert np.array_equal(bits32(ys[1]), want) and np.array_equal(bits32(ys[0]), want[:1000])
+
+
+def test_batched_decode_validates_pairs(efl):
+    M = torch.zeros(8, dtype=torch.int64, device="cuda")
+    E = torch.zeros(8, dtype=torch.int64, device="cuda")
+    with pytest.raises(efl.errors.InvalidArgumentError, match="same size"):
+        efl.lib.ops.fixed_point_to_float_point_batched([M], [E[:7]])
+    with pytest.raises(efl.errors.InvalidArgumentError, match="int64"):
+        efl.lib.ops.fixed_point_to_float_point_batched([M.int()], [E])
+    with pytest.raises(efl.errors.InvalidArgumentError, match="as many"):
+        efl.lib.ops.fixed_point_to_float_point_batched([M, M], [E])
+    # a strided view decodes its own elements
+    Mb = torch.arange(16, dtype=torch.int64, device="cuda") + 1
+    Eb = torch.zeros(16, dtype=torch.int64, device="cuda")
+    (y,) = efl.lib.ops.fixed_point_to_float_point_batched([Mb[::2]], [Eb[::2]])
+    assert torch.equal(y.cpu(), torch.arange(1, 17, 2, dtype=torch.float32))
+
+
 # ---------------------------------------------------------------- seeded inputs vs oracle
 
 SIZES = [0, 1, 2, 3, 5, 127, 255, 256, 1023, 4097, 65537, (1 << 20) + 3]
@@ -263,9 +309,12 @@ def test_full_size_properties(efl):
     fp = efl.paillier.fixedpoint.encode(x)
     y = efl.paillier.fixedpoint.decode(fp)
     nz = x != 0
-    # round trip is the identity on every non-zero N(0,1) value; zeros become 2^-127
-    assert torch.equal(y[nz], x[nz])
-    assert torch.all(y[~nz].view(torch.int32) == 0x00400000)
+    # default (FTZ, the op as TF runs it): the round trip is the identity on every bit pattern
+    assert torch.equal(y.view(torch.int32), x.view(torch.int32))
+    # bare loop: identity on every non-zero N(0,1) value; zeros become 2^-127
+    y0 = efl.lib.ops.fixed_point_to_float_point(fp.mantissa, fp.exponent, flush_denormal=False)
+    assert torch.equal(y0[nz], x[nz])
+    assert torch.all(y0[~nz].view(torch.int32) == 0x00400000)
     # mantissas are odd (normalised) except the zero quirk, |M| < 2^24
     M, E = fp.mantissa, fp.exponent
     assert torch.all((M[nz] & 1) == 1) and torch.all(M.abs() < (1 << 24))

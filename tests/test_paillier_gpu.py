@@ -154,6 +154,30 @@ def test_round_trip_and_counter_advance(efl):
     assert d.shape == (33, 7) and [int(s, 16) for s in d.strings()] == m.reshape(-1).tolist()
 
 
+def test_mixed_hsa_never_reuses_a(efl):
+    """encrypt with some hsa given and some "0", then default encrypts and a Philox
+    fbpowm: every freshly drawn hs^a is distinct (m = 0 makes the ciphertext equal hs^a), and the
+    zero-hsa rows draw the counter of their own index."""
+    k = ENC_KEYS[0]
+    kp = keypair(efl, k, seed=4321)
+    N = 40
+    zero_rows = [0, 1, 2, 7, 20, 21, 39]
+    given = kp.fbpowm(a=[12345 + i for i in range(N)]).to_hex().strings()
+    hsa = ["0" if i in zero_rows else given[i] for i in range(N)]
+    c1 = kp.encrypt(torch.zeros(N, dtype=torch.int64), hsa=hsa).tensor.to_hex().strings()
+    for i in range(N):
+        if i not in zero_rows:
+            assert c1[i] == given[i]
+    okp = P.Keypair(int(k["n"], 16), int(k["hs"], 16), k["a_bits"] // 8, 1)
+    for i in zero_rows:   # row i of the call took counter 0 + i
+        assert c1[i] == P.hx(P.fbpowm(okp.hs, okp.n2, philox.draw_a(kp.seed, i, k["a_bits"]), 1))
+    c2 = kp.encrypt(torch.zeros(N, dtype=torch.int64)).tensor.to_hex().strings()
+    c3 = kp.fbpowm(n=N).to_hex().strings()
+    fresh = [c1[i] for i in zero_rows] + c2 + c3
+    assert len(set(fresh)) == len(fresh)
+    assert kp.counter == 3 * N
+
+
 def test_errors(efl):
     k = ENC_KEYS[0]
     pub = keypair(efl, k, private=False)

@@ -1,0 +1,29 @@
+#!/bin/bash
+# Round-2 GPU session script: each GPU step under its own time limit, chained with &&, output
+# under gpurun_out/. Usage: bash tools/gpu_r02.sh <step>...  (steps: tests, probe, bench, bench2,
+# prof, pmc)
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+export PYTHONUNBUFFERED=1
+run() {
+  case "$1" in
+    tests)  timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+              > gpurun_out/pytest.log 2>&1 ;;
+    dist)   timeout -k 10 200 python -u -m pytest tests/test_distributed_gpu.py -m gpu -x -v --timeout 150 \
+              --timeout-method thread > gpurun_out/pytest_dist.log 2>&1 ;;
+    probe)  timeout -k 10 240 python -u tools/step_probe.py > gpurun_out/step_probe.json 2> gpurun_out/step_probe.err ;;
+    bench)  timeout -k 10 300 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err ;;
+    bench2) timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+              --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 3 \
+              > gpurun_out/bench2.json 2> gpurun_out/bench2.err ;;
+    prof)   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- \
+              python3 bench.py --no-extras --no-cpu-baseline > gpurun_out/bench_prof.json 2> gpurun_out/prof.err ;;
+    *) echo "unknown step $1"; return 2 ;;
+  esac
+}
+for s in "$@"; do
+  echo "== $s $(date +%T)"
+  run "$s" || { rc=$?; echo "step $s failed rc=$rc"; exit $rc; }
+done
+echo "== done $(date +%T)"
