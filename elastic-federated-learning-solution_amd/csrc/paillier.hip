@@ -120,33 +120,24 @@ __device__ __forceinline__ void make_g(uint32_t (&g)[2 * LN], long long m, const
 }
 
 // ------------------------------------------------------------------------------------------
-// fixed-base exponentiation hs^(a') mod n^2 through the table (gmp_utils.cc:107-144):
-// groups of g bits of a, each group's index built MSB-first from its LOW bit; the top partial
-// group likewise. Table entries T[i][j] = hs^((j+1) 2^(g i)) in Montgomery form.
-// Returns acc = hs^(a') * R mod n^2 (Montgomery form).
+// fixed-base exponentiation hs^(a') mod n^2 through the table (gmp_utils.cc:107-144): a' = a with
+// every group_size-bit group bit-reversed (the reference's index order, pl_common.h), formed in
+// place in the lane's column, then taken in plain windows of the table's width W. Table entries
+// T[i][j] = hs^((j+1) 2^(W i)) in Montgomery form. Returns acc = hs^(a') * R mod n^2.
 // ------------------------------------------------------------------------------------------
 template <int LC>
-__device__ __forceinline__ void fbpowm_mont(uint32_t (&acc)[LC], const Key& k, const uint32_t* acol,
+__device__ __forceinline__ void fbpowm_mont(uint32_t (&acc)[LC], const Key& k, uint32_t* acol,
                                             uint32_t* bcol, int S) {
-  const int g = k.d.group_size;
   const int words = (k.d.a_bits + 31) >> 5;
-  // bit length of a
-  int size = 0;
-  for (int w = words - 1; w >= 0; --w) {
-    const uint32_t v = acol[w * S];
-    if (v) { size = w * 32 + 32 - __clz(v); break; }
-  }
+  const int size = pl::col_bit_length(acol, S, words);
+  pl::regroup_exponent(acol, S, size, k.d.group_size, words);
+  const int W = pl::table_window(k.d);
   load_uniform<LC>(acc, k.at(k.d.off_n2_one));
   const uint32_t* n2 = k.at(k.d.off_n2);
   const uint32_t* table = k.at(k.d.off_table);
   const int cols = k.d.table_cols;
-  for (int s = 0, row = 0; s < size; s += g, ++row) {
-    const int w = size - s < g ? size - s : g;
-    uint32_t idx = 0;
-    for (int j = 0; j < w; ++j) {
-      const int b = s + j;
-      idx = (idx << 1) | ((acol[(b >> 5) * S] >> (b & 31)) & 1u);
-    }
+  for (int s = 0, row = 0; s < size; s += W, ++row) {
+    const uint32_t idx = pl::col_bits(acol, S, s, size - s < W ? size - s : W, words);
     if (idx) {
       g_to_lds<LC>(bcol, S, table + ((int64_t)row * cols + (idx - 1)) * LC);
       mont_mul<LC>(acc, LdsCol{bcol, S}, n2, k.d.n2_minv);
@@ -854,6 +845,23 @@ inline bool key_ok(const efl_pl_key* d, bool need_private, int ln_max) {
   return true;
 }
 
+// the fixed-base table covers a: W-bit windows (1..24), 2^W - 1 columns, ceil(a_bits / W) rows;
+// group_size (the API's, used to form a') in 1..32
+inline int table_ok(const efl_pl_key* d) {
+  const int W = d->table_window > 0 ? d->table_window : d->group_size;
+  if (d->table_rows <= 0 || d->group_size <= 0) {
+    set_error("no fixed-base table: set the public key first");
+    return EFL_E_ABORTED;
+  }
+  if (W < 1 || W > 24 || d->group_size > 32 || d->table_cols != (1 << W) - 1 ||
+      (int64_t)d->table_rows * W < d->a_bits) {
+    set_error("fixed-base table %d x %d (window %d) does not cover %d-bit exponents", d->table_rows,
+              d->table_cols, W, d->a_bits);
+    return EFL_E_INVALID_ARGUMENT;
+  }
+  return EFL_OK;
+}
+
 // kernel family per key size: 0 = one lane per element (paillier.hip), C = sliced over 2ln/C (n^2
 // ops) or ln/C (decryption) lanes of C limbs (paillier_sliced.hip). [ln 16/32/64/128][n^2 ops, decrypt]
 constexpr int kDefaultSlicing[4][2] = {{16, 8}, {16, 32}, {16, 32}, {8, 32}};   // measured: profiles/r01/bench_pl*.jsonl
@@ -961,9 +969,9 @@ EFL_API int efl_pl_encrypt(const void* key_block, const efl_pl_key* key, const i
   if (!key_ok(key, false, 128)) return EFL_E_INVALID_ARGUMENT;
   if (n < 0) { set_error("negative count"); return EFL_E_INVALID_ARGUMENT; }
   if (n == 0) return EFL_OK;
-  if (!hsa && (key->table_rows <= 0 || key->group_size <= 0)) {
-    set_error("no fixed-base table: set the public key first");
-    return EFL_E_ABORTED;
+  if (!hsa) {
+    const int rc = table_ok(key);
+    if (rc != EFL_OK) return rc;
   }
   Key k{(const uint32_t*)key_block, *key};
   const int C = slicing(key->ln, 0);
@@ -978,6 +986,8 @@ EFL_API int efl_pl_fbpowm(const void* key_block, const efl_pl_key* key, const ui
                           int64_t n, uint64_t seed, int64_t counter_base, void* stream) {
   if (!key_ok(key, false, 128)) return EFL_E_INVALID_ARGUMENT;
   if (n <= 0) return n < 0 ? EFL_E_INVALID_ARGUMENT : EFL_OK;
+  const int rc = table_ok(key);
+  if (rc != EFL_OK) return rc;
   Key k{(const uint32_t*)key_block, *key};
   const int C = slicing(key->ln, 0);
   return hip_status(C ? pl::sl_fbpowm(k, C, a, hsa, (long long)n, seed, (long long)counter_base, (hipStream_t)stream)

@@ -93,27 +93,29 @@ __device__ __forceinline__ void make_g(uint32_t (&t)[C], long long m, const Key&
   add_small<C, G>(t, 1u, g);
 }
 
+// a -> a' (pl_common.h regroup_exponent) on the element's group leader, then every lane of the
+// group sees it; returns a's bit length
+__device__ __forceinline__ int regroup_shared(uint32_t* A, int E, int words, int gs, int g) {
+  const int size = col_bit_length(A, E, words);
+  if (gs > 1) {
+    if (g == 0) regroup_exponent(A, E, size, gs, words);
+    lds_sync();
+  }
+  return size;
+}
+
 // hs^(a') R mod n^2 through the fixed-base table (gmp_utils.cc:107-144; see paillier.hip)
 template <int C, int G>
-__device__ __forceinline__ void fbpowm_mont(uint32_t (&acc)[C], const Key& k, const uint32_t* A, uint32_t* B, int E,
+__device__ __forceinline__ void fbpowm_mont(uint32_t (&acc)[C], const Key& k, uint32_t* A, uint32_t* B, int E,
                                             int words, const uint32_t (&n2)[C], int g) {
   constexpr int L = C * G;
-  const int gs = k.d.group_size;
-  int size = 0;
-  for (int w = words - 1; w >= 0; --w) {
-    const uint32_t v = A[w * E];
-    if (v) { size = w * 32 + 32 - __clz(v); break; }
-  }
+  const int size = regroup_shared(A, E, words, k.d.group_size, g);
+  const int W = table_window(k.d);
   slice_uniform<C>(acc, k.at(k.d.off_n2_one), g);
   const uint32_t* table = k.at(k.d.off_table);
   const int cols = k.d.table_cols;
-  for (int s = 0, row = 0; s < size; s += gs, ++row) {
-    const int w = size - s < gs ? size - s : gs;
-    uint32_t idx = 0;
-    for (int j = 0; j < w; ++j) {
-      const int b = s + j;
-      idx = (idx << 1) | ((A[(b >> 5) * E] >> (b & 31)) & 1u);
-    }
+  for (int s = 0, row = 0; s < size; s += W, ++row) {
+    const uint32_t idx = col_bits(A, E, s, size - s < W ? size - s : W, words);
     if (idx) {
       uint32_t ent[C];
       load_slice<C>(ent, table + ((int64_t)row * cols + (idx - 1)) * L, g);
@@ -207,29 +209,20 @@ __global__ __launch_bounds__(kSlBlock) SL_OCC void k_fbpowm(Key k, const uint32_
 // hs^(a') mod n^2 through the radix-2^28 table (same lookup order as fbpowm_mont), result in
 // NORMAL form as this lane's C 32-bit words. Scratch: B (entry / conversion, L28 words per element).
 template <int C, int G>
-__device__ __forceinline__ void fbpowm28(uint32_t (&out)[C], const Key& k, const uint32_t* A, uint32_t* B, int E,
+__device__ __forceinline__ void fbpowm28(uint32_t (&out)[C], const Key& k, uint32_t* A, uint32_t* B, int E,
                                          int words, int g) {
   constexpr int L = C * G;
   constexpr int C28 = s28::limbs_per_lane(L, G), L28 = C28 * G;
-  const int gs = k.d.group_size;
-  int size = 0;
-  for (int w = words - 1; w >= 0; --w) {
-    const uint32_t v = A[w * E];
-    if (v) { size = w * 32 + 32 - __clz(v); break; }
-  }
+  const int size = regroup_shared(A, E, words, k.d.group_size, g);
+  const int W = table_window(k.d);
   uint32_t m28[C28], acc[C28];
   slice_uniform<C28>(m28, k.at(k.d.off_n2_28), g);
   slice_uniform<C28>(acc, k.at(k.d.off_n2_one28), g);
   const uint32_t minv28 = k.d.n2_minv28;
   const uint32_t* table = k.at(k.d.off_table28);
   const int cols = k.d.table_cols;
-  for (int s = 0, row = 0; s < size; s += gs, ++row) {
-    const int w = size - s < gs ? size - s : gs;
-    uint32_t idx = 0;
-    for (int j = 0; j < w; ++j) {
-      const int b = s + j;
-      idx = (idx << 1) | ((A[(b >> 5) * E] >> (b & 31)) & 1u);
-    }
+  for (int s = 0, row = 0; s < size; s += W, ++row) {
+    const uint32_t idx = col_bits(A, E, s, size - s < W ? size - s : W, words);
     if (idx) {
       const uint32_t* ent = table + ((int64_t)row * cols + (idx - 1)) * L28 + g * C28;
 #pragma unroll

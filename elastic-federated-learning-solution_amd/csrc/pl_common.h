@@ -30,6 +30,60 @@ __device__ __forceinline__ void philox(uint32_t (&c)[4], uint32_t k0, uint32_t k
   }
 }
 
+// ---- the fixed-base exponent (FixedBasePowm, gmp_utils.cc:107-144) --------------------------
+// An element's exponent a lives as `words` little-endian 32-bit words in an LDS column of stride
+// S. The reference's mpz_fbpowm builds each g-bit group's table index MSB-first from the group's
+// LOW bit (the top group is as wide as a's remaining bit length), so what it computes is hs^(a'),
+// a' = a with every group bit-reversed. The kernels form a' in place
+// with the API group size and then walk a' in plain windows of the table's OWN width
+// (efl_pl_key.table_window): the result is the same group element for any window, and the window
+// only sets the cost (one product per non-zero window).
+
+// bits [s, s + w) of the column's number, 1 <= w <= 32
+__device__ __forceinline__ uint32_t col_bits(const uint32_t* col, int S, int s, int w, int words) {
+  const int q = s >> 5, r = s & 31;
+  uint64_t v = col[q * S];
+  if (r + w > 32 && q + 1 < words) v |= (uint64_t)col[(q + 1) * S] << 32;
+  return (uint32_t)(v >> r) & (uint32_t)((1ull << w) - 1ull);
+}
+
+__device__ __forceinline__ void col_put_bits(uint32_t* col, int S, int s, int w, uint32_t val, int words) {
+  const int q = s >> 5, r = s & 31;
+  const bool two = r + w > 32 && q + 1 < words;
+  uint64_t v = col[q * S];
+  if (two) v |= (uint64_t)col[(q + 1) * S] << 32;
+  const uint64_t mask = ((1ull << w) - 1ull) << r;
+  v = (v & ~mask) | (((uint64_t)val << r) & mask);
+  col[q * S] = (uint32_t)v;
+  if (two) col[(q + 1) * S] = (uint32_t)(v >> 32);
+}
+
+// bit length of the column's number
+__device__ __forceinline__ int col_bit_length(const uint32_t* col, int S, int words) {
+  for (int w = words - 1; w >= 0; --w) {
+    const uint32_t v = col[w * S];
+    if (v) return w * 32 + 32 - __clz(v);
+  }
+  return 0;
+}
+
+// a -> a' in place: every g-bit group of a's `size` bits (the top one `size mod g` wide)
+// bit-reversed. g == 1 is the identity.
+__device__ __forceinline__ void regroup_exponent(uint32_t* col, int S, int size, int g, int words) {
+  if (g <= 1) return;
+  for (int s = 0; s < size; s += g) {
+    const int w = size - s < g ? size - s : g;
+    const uint32_t v = col_bits(col, S, s, w, words);
+    col_put_bits(col, S, s, w, __brev(v) >> (32 - w), words);
+  }
+}
+
+// width of the table's windows (0 in a descriptor from before the field existed: the API group
+// size, whose table is the same T[i][j] = hs^((j+1) 2^(g i)))
+__device__ __forceinline__ int table_window(const efl_pl_key& d) {
+  return d.table_window > 0 ? d.table_window : d.group_size;
+}
+
 // Sliced kernels (paillier_sliced.hip): one number over L/C lanes of C limbs. L = limbs of the
 // modulus the op works in (2*ln for n^2 ops, ln for decryption's p^2 / q^2).
 bool sliced_available(int L, int C);

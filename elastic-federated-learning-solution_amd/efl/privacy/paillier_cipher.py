@@ -45,7 +45,7 @@ class PlKey(ctypes.Structure):
                 ("off_p2_r2_28", ctypes.c_int64 * 6), ("off_q2_r2_28", ctypes.c_int64 * 6),
                 ("n2_28_len", ctypes.c_int32), ("table28_log2g", ctypes.c_int32), ("n2_minv28", ctypes.c_uint32),
                 ("off_n2_28", ctypes.c_int64), ("off_n2_one28", ctypes.c_int64), ("off_table28", ctypes.c_int64),
-                ("off_n2_r2_28", ctypes.c_int64)]
+                ("off_n2_r2_28", ctypes.c_int64), ("table_window", ctypes.c_int32)]
 
 
 _PK = ctypes.POINTER(PlKey)
@@ -110,6 +110,22 @@ def _limbs28_rows(vals, L: int, nbytes: int) -> np.ndarray:
         bits = np.pad(bits, ((0, 0), (0, need - bits.shape[1])))
     w = (1 << np.arange(28, dtype=np.uint32)).astype(np.uint32)
     return (bits[:, :need].reshape(len(vals), L, 28).astype(np.uint32) * w).sum(axis=2, dtype=np.uint32)
+
+
+TABLE_MAX_ENTRIES = 1 << 18   # per key: 2^18 entries = 256 MiB of 4096-bit (8192-bit n^2) words
+
+
+def choose_table_window(a_bits: int, max_entries: int = TABLE_MAX_ENTRIES) -> int:
+    """Widest window W whose table (ceil(a_bits / W) rows x 2^W - 1 entries) stays within
+    max_entries: a fresh-randomness encryption costs ceil(a_bits / W) (1 - 2^-W) products, so the
+    widest affordable window is the fastest. 2048-bit a (the reference default) -> W = 10,
+    512-bit a (the examples) -> W = 12."""
+    best = 1
+    for W in range(1, 17):
+        if -(-a_bits // W) * ((1 << W) - 1) > max_entries:
+            break
+        best = W
+    return best
 
 
 def _limbs(x: int, L: int) -> np.ndarray:
@@ -214,7 +230,8 @@ def generate_keypair_ints(n_bytes=512, reps=24, rng=None):
 class KeyBlock:
     """Host derivation + device upload of every constant the kernels read (efl_pl_key)."""
 
-    def __init__(self, n: int, hs: int, a_bits: int, group_size: int, p=None, q=None, device=None):
+    def __init__(self, n: int, hs: int, a_bits: int, group_size: int, p=None, q=None, device=None,
+                 table_window=None, reuse_table=None):
         if n.bit_length() < 128:
             raise errors.UnimplementedError("n of fewer than 128 bits is not supported on the GPU")
         if p is not None and q is not None and q >= 2 * p:
@@ -285,61 +302,122 @@ class KeyBlock:
             for k, L28 in enumerate(L28s):
                 d.off_p2_r2_28[k] = put28(pow(2, 2 * 28 * L28, p * p))
                 d.off_q2_r2_28[k] = put28(pow(2, 2 * 28 * L28, q * q))
-        # fixed-base table T[i][j] = hs^((j+1) 2^(g i)) mod n^2, Montgomery form (gmp_utils.cc:56-89)
+        # Fixed-base table (gmp_utils.cc:56-89). The reference builds T[i][j] = hs^((j+1) 2^(g i))
+        # with its API group size g and reads it with per-group bit-reversed indices, i.e. it
+        # computes hs^(a'), a' = a with every g-bit group reversed. The kernels form a' themselves
+        # (pl_common.h regroup_exponent) and walk it in plain windows of THIS table's width W,
+        # chosen here for speed: one Montgomery product per non-zero window, so W = 10 cuts the
+        # reference default (4096-bit n, g = 1, 2048-bit a) from ~1024 products per encryption
+        # to ~205. The reference's size guard still applies to the table it would build.
         g = group_size
-        cols = (1 << g) - 1
-        rows = a_bits // g + (1 if a_bits % g else 0)
-        if rows * cols * n2.bit_length() > MAX_TABLE_BITS:
+        api_rows = a_bits // g + (1 if a_bits % g else 0)
+        if api_rows * ((1 << g) - 1) * n2.bit_length() > MAX_TABLE_BITS:
             raise errors.ResourceExhaustedError("Memory usage exceeds a predefined threshold.")
-        d.table_rows, d.table_cols = rows, cols
+        W = int(table_window) if table_window else choose_table_window(a_bits)
+        if not 1 <= W <= 16:
+            raise errors.InvalidArgumentError("table_window must be in [1, 16]")
+        cols = (1 << W) - 1
+        rows = -(-a_bits // W)
+        d.table_rows, d.table_cols, d.table_window = rows, cols, W
+        self.table_window = W
         # radix-2^28 copy for the sliced family the n^2 kernels use (include/efl_hip.h)
         d.off_table28 = -1
         fam = kernel_slicing(ln, False)
-        tab28 = None
+        L28 = 0
         if fam:
             G = 2 * ln // fam
             L28 = limbs28_total(2 * ln, G)
             if rows * cols * L28 * 4 <= TABLE28_MAX_BYTES:
                 R28 = 1 << (28 * L28)
-                nb28 = (28 * L28 + 7) // 8
                 d.n2_28_len, d.table28_log2g = L28, G.bit_length() - 1
                 d.n2_minv28 = (-pow(n2, -1, 1 << 28)) % (1 << 28)
-                tab28 = np.empty((rows, cols, L28), dtype="<u4")
-        d.off_table = pos[0]
-        entry = hs % n2
-        row = []
-        acc = entry
-        for j in range(cols):                 # row 0: hs^1 .. hs^cols
-            row.append(acc)
-            acc = acc * entry % n2
-        tab = np.empty((rows, cols, self.lc), dtype="<u4")
-        nbytes = 4 * self.lc
-        for i in range(rows):
-            if i:
-                sq = 1 << g
-                row = [pow(v, sq, n2) for v in row]
-            buf = b"".join((v * Rc % n2).to_bytes(nbytes, "little") for v in row)
-            tab[i] = np.frombuffer(buf, dtype="<u4").reshape(cols, self.lc)
-            if tab28 is not None:
-                tab28[i] = _limbs28_rows([v * R28 % n2 for v in row], L28, nb28)
-        words.append(tab.reshape(-1))
-        pos[0] += tab.size
-        if tab28 is not None:
-            d.off_n2_28 = pos[0]
-            words.append(_limbs28(n2, L28))
-            pos[0] += L28
-            d.off_n2_one28 = pos[0]
-            words.append(_limbs28(R28 % n2, L28))
-            pos[0] += L28
-            d.off_n2_r2_28 = pos[0]
-            words.append(_limbs28(R28 * R28 % n2, L28))
-            pos[0] += L28
-            d.off_table28 = pos[0]
-            words.append(tab28.reshape(-1))
-            pos[0] += tab28.size
-        host = np.concatenate(words)
-        self.block = torch.from_numpy(host.view(np.int32)).to(self.device)
+                d.off_n2_28 = pos[0]
+                words.append(_limbs28(n2, L28))
+                pos[0] += L28
+                d.off_n2_one28 = pos[0]
+                words.append(_limbs28(R28 % n2, L28))
+                pos[0] += L28
+                d.off_n2_r2_28 = pos[0]
+                words.append(_limbs28(R28 * R28 % n2, L28))
+                pos[0] += L28
+                r28_one = put(R28 % n2, self.lc)          # R28 mod n^2 as 32-bit words (table build)
+            else:
+                L28 = 0
+        r_one = d.off_n2_one
+        head = torch.from_numpy(np.concatenate(words).view(np.int32)).to(self.device)
+        # the key block without its tables runs the build (n^2 powm / multiply kernels)
+        d.off_table = -1
+        saved = (d.table_rows, d.off_table28)
+        d.table_rows, d.off_table28 = 0, -1
+        self.block, self.ptr = head, head.data_ptr()
+        src = reuse_table
+        if src is not None and (src.n, src.hs, src.a_bits, src.table_window, src.lc) == (n, hs, a_bits, W, self.lc) \
+                and (src.desc.off_table28 >= 0) == bool(L28) and (not L28 or src.desc.n2_28_len == L28):
+            # set_private_key on a key whose public part is unchanged: the tables are the same
+            o32, o28 = src.desc.off_table, src.desc.off_table28
+            t32 = src.block[o32:o32 + rows * cols * self.lc]
+            t28 = src.block[o28:o28 + rows * cols * L28] if L28 else None
+        else:
+            t32, t28 = self._build_table(hs % n2, n2, W, rows, cols, head, r_one, r28_one if L28 else None, L28)
+        d.table_rows, d.off_table28 = saved
+        parts = [head, t32.reshape(-1)]
+        d.off_table = head.numel()
+        if L28:
+            d.off_table28 = head.numel() + t32.numel()
+            parts.append(t28.reshape(-1))
+        self.block = torch.cat(parts)
         self.ptr = self.block.data_ptr()
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def _build_table(self, hs, n2, W, rows, cols, head, r_one, r28_one, L28, chunk_entries=1 << 16):
+        """T[i][j-1] = hs^(j 2^(W i)) mod n^2 for j in 1..2^W-1, in Montgomery form (x R mod n^2,
+        [rows, cols, 2 ln] words) and, with L28, radix-2^28 Montgomery form (x R28 mod n^2,
+        [rows, cols, L28] limbs). Row bases hs^(2^(W i)) come from W squarings each on the host;
+        every entry is then one short GPU exponentiation base_i^j (efl_pl_powm, W-bit exponents)
+        and one GPU product by R (or R28) mod n^2 (efl_pl_add) — the work the reference does with
+        mpz_mul per entry when a keypair is set (gmp_utils.cc:73-88)."""
+        dev, lc = self.device, self.lc
+        sh = _stream(dev)
+        bases = []
+        b = hs
+        for i in range(rows):
+            bases.append(b)
+            if i + 1 < rows:
+                b = pow(b, 1 << W, n2)
+        bases_d = torch.from_numpy(np.stack([_limbs(v, lc) for v in bases]).view(np.int32)).to(dev)
+        t32 = torch.empty((rows, cols, lc), dtype=torch.int32, device=dev)
+        t28 = torch.empty((rows, cols, L28), dtype=torch.int32, device=dev) if L28 else None
+        exps = torch.arange(1, cols + 1, dtype=torch.int32, device=dev)
+        rows_per = max(1, chunk_entries // cols)
+        d = self.desc
+        one = head[r_one:r_one + lc]
+        one28 = head[r28_one:r28_one + lc] if L28 else None
+        if L28:
+            q, r = divmod(np.arange(L28) * 28, 32)
+            qi = torch.from_numpy(q).to(dev)
+            rs = torch.from_numpy(r).to(dev)
+        for r0 in range(0, rows, rows_per):
+            r1 = min(rows, r0 + rows_per)
+            N = (r1 - r0) * cols
+            X = bases_d[r0:r1].unsqueeze(1).expand(r1 - r0, cols, lc).reshape(N, lc).contiguous()
+            E = exps.repeat(r1 - r0).reshape(N, 1).contiguous()
+            T = torch.empty_like(X)
+            _efl_lib.check(_lib.efl_pl_powm(head.data_ptr(), ctypes.byref(d), X.data_ptr(), E.data_ptr(), 1,
+                                            T.data_ptr(), N, sh))
+            Y = one.expand(N, lc).contiguous()
+            _efl_lib.check(_lib.efl_pl_add(head.data_ptr(), ctypes.byref(d), T.data_ptr(), Y.data_ptr(),
+                                           t32[r0:r1].data_ptr(), N, sh))
+            if L28:
+                Y.copy_(one28.expand(N, lc))
+                _efl_lib.check(_lib.efl_pl_add(head.data_ptr(), ctypes.byref(d), T.data_ptr(), Y.data_ptr(),
+                                               X.data_ptr(), N, sh))
+                # x R28 mod n^2 < 2^(32 lc): words past lc (up to the last limb's + 1) are zero
+                pad = int(q.max()) + 2 - lc
+                w = torch.cat([X.to(torch.int64) & 0xFFFFFFFF,
+                               torch.zeros((N, max(1, pad)), dtype=torch.int64, device=dev)], dim=1)
+                limbs = ((w[:, qi] >> rs) | (w[:, qi + 1] << (32 - rs))) & 0xFFFFFFF
+                t28[r0:r1] = limbs.to(torch.int32).reshape(r1 - r0, cols, L28)
+        return t32, t28
 
     def args(self):
         return self.ptr, ctypes.byref(self.desc)
@@ -502,12 +580,14 @@ class PaillierKeypair(object):
         self._set(k.n, self._n_bytes, k.hs, k.a_bits // 8, k.group_size,
                   int(_hex_of(p), 16), int(_hex_of(q), 16))
 
-    def set_keys_ints(self, n, hs, a_bytes, group_size=1, p=None, q=None, n_bytes=None):
-        """Host-int variant of set_public_key/set_private_key (tests, key exchange)."""
-        self._set(n, n_bytes or (n.bit_length() + 7) // 8, hs, a_bytes, group_size, p, q)
+    def set_keys_ints(self, n, hs, a_bytes, group_size=1, p=None, q=None, n_bytes=None, table_window=None):
+        """Host-int variant of set_public_key/set_private_key (tests, key exchange). table_window
+        forces the fixed-base table's window (default: choose_table_window; results never change)."""
+        self._set(n, n_bytes or (n.bit_length() + 7) // 8, hs, a_bytes, group_size, p, q, table_window)
 
-    def _set(self, n, n_bytes, hs, a_bytes, group_size, p=None, q=None):
-        self._key = KeyBlock(n, hs, 8 * int(a_bytes), int(group_size), p, q)
+    def _set(self, n, n_bytes, hs, a_bytes, group_size, p=None, q=None, table_window=None):
+        self._key = KeyBlock(n, hs, 8 * int(a_bytes), int(group_size), p, q, table_window=table_window,
+                             reuse_table=self._key)
         self._n_bytes = n_bytes
 
     @property

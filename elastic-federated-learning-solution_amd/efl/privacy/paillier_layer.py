@@ -241,21 +241,71 @@ def _row(c, i):
     return CipherTensor(c.limbs[i * cols:(i + 1) * cols].contiguous(), (cols,), c.key)
 
 
+# ----------------------------------------------------------------------------------------------
+# functional forms. TF1 runs them once, while building the graph, and tf.layers keeps their
+# variables by scope name (`name`, `_reuse`, paillier_layer.py:166-203). Eagerly they run every
+# step, so each layer (and the receiver's plaintext Dense) is built once per (communicator,
+# function, prefix, name) and found again on later calls: its weights persist and train.
+# ----------------------------------------------------------------------------------------------
+
+def cached_layers(communicator) -> dict:
+    """The layers the functional forms built on `communicator`, keyed (function, prefix, name);
+    collect their parameters for the optimizer from here."""
+    reg = getattr(communicator, "_efl_paillier_layers", None)
+    if reg is None:
+        reg = {}
+        setattr(communicator, "_efl_paillier_layers", reg)
+    return reg
+
+
+def _cached(communicator, key, build):
+    reg = cached_layers(communicator)
+    layer = reg.get(key)
+    if layer is None:
+        layer = reg[key] = build()
+    return layer
+
+
+def _plain_dense(in_features, units, use_bias, kernel_initializer, bias_initializer, device):
+    """tf.layers.Dense(units) of the receiver's own features: kernel glorot-uniform (TF's default)
+    unless kernel_initializer is given (a callable filling a [in, units] tensor in place, TF's
+    orientation), bias zeros unless bias_initializer is given."""
+    lin = torch.nn.Linear(in_features, units, bias=use_bias)
+    with torch.no_grad():
+        w = torch.empty(in_features, units)
+        if kernel_initializer is None:
+            torch.nn.init.xavier_uniform_(w)
+        else:
+            kernel_initializer(w)
+        lin.weight.copy_(w.t())
+        if use_bias:
+            if bias_initializer is None:
+                lin.bias.zero_()
+            else:
+                bias_initializer(lin.bias)
+    return lin.to(device)
+
+
 @exporter.export("paillier.sender.dense")
 def dense_send(inputs, keypair, communicator, prefix, units, name=None, reuse=None, seed=None):
-    layer = PaillierActiveDense(keypair, communicator, prefix, units, name=name, _reuse=reuse, seed=seed)
+    layer = _cached(communicator, ("sender.dense", prefix, name),
+                    lambda: PaillierActiveDense(keypair, communicator, prefix, units, name=name, _reuse=reuse,
+                                                seed=seed))
     return layer(inputs), layer.kernel
 
 
 @exporter.export("paillier.recver.dense")
 def dense_recv(inputs, keypair, communicator, prefix, recv_shape, units, activation=None, use_bias=True,
-               kernel_initializer=None, name=None, reuse=None, seed=None, **_unused):
-    layer = PaillierPassiveDense(keypair, communicator, prefix, units, kernel_initializer=kernel_initializer,
-                                 seed=seed)
+               kernel_initializer=None, bias_initializer=None, name=None, reuse=None, seed=None, **_unused):
+    layer = _cached(communicator, ("recver.dense", prefix, name),
+                    lambda: PaillierPassiveDense(keypair, communicator, prefix, units,
+                                                 kernel_initializer=kernel_initializer, seed=seed))
     x_exponent = communicator.recv(prefix + "_[x]_exponent", shape=recv_shape, dtype=torch.int64)
     y = layer(x_exponent.to(_device_of(inputs)))
     if inputs is not None:
-        lin = torch.nn.Linear(inputs.shape[-1], units, bias=use_bias).to(inputs.device)
+        lin = _cached(communicator, ("recver.dense.plain", prefix, name),
+                      lambda: _plain_dense(inputs.shape[-1], units, use_bias, kernel_initializer,
+                                           bias_initializer, inputs.device))
         y = y + lin(inputs)
     if activation is not None:
         y = activation(y)
@@ -264,14 +314,16 @@ def dense_recv(inputs, keypair, communicator, prefix, recv_shape, units, activat
 
 @exporter.export("paillier.sender.weight")
 def weight_send(inputs, keypair, communicator, prefix, units, seed=None):
-    layer = PaillierActiveWeight(keypair, communicator, prefix, units, seed=seed)
+    layer = _cached(communicator, ("sender.weight", prefix, None),
+                    lambda: PaillierActiveWeight(keypair, communicator, prefix, units, seed=seed))
     return layer(inputs), layer.kernel
 
 
 @exporter.export("paillier.recver.weight")
 def weight_recv(inputs, keypair, communicator, prefix, units, kernel_initializer=None, seed=None):
-    layer = PaillierPassiveWeight(keypair, communicator, prefix, units, kernel_initializer=kernel_initializer,
-                                  seed=seed)
+    layer = _cached(communicator, ("recver.weight", prefix, None),
+                    lambda: PaillierPassiveWeight(keypair, communicator, prefix, units,
+                                                  kernel_initializer=kernel_initializer, seed=seed))
     x_exponent = communicator.recv(prefix + "_[x]_exponent", shape=(-1, units), dtype=torch.int64)
     y = layer(x_exponent.to(_device_of(inputs)))
     if inputs is not None:

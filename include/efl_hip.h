@@ -135,7 +135,8 @@ int efl_fxp_decode_batched(const int64_t* const* mantissas, const int64_t* const
  *   n2_minv      -n^2^-1 mod 2^32 (Montgomery), likewise p2_/q2_/p_/q_minv.
  *   off_n2_r2    R^2 mod n^2, R = 2^(32*2*ln);  off_n2_one  R mod n^2
  *   off_table    fbpowm table, table_rows x table_cols entries of 2*ln limbs, entry [i][j] =
- *                hs^((j+1) * 2^(group_size*i)) * R mod n^2 (gmp_utils.cc:56-89, Montgomery form)
+ *                hs^((j+1) * 2^(W*i)) * R mod n^2, W = table_window (gmp_utils.cc:56-89 with its
+ *                own window; Montgomery form)
  *   off_p2_r3    R'^3 mod p^2, R' = 2^(32*ln) (and q2)
  *   off_pm1      exponent p-1 (ln/2 limbs, pm1_bits significant bits), likewise q-1
  *   off_pinv_w   p^-1 mod 2^(32*ln/2) (exact division by p), likewise q
@@ -172,13 +173,19 @@ typedef struct {
    *   off_n2_28     n^2 as L28 28-bit limbs; n2_minv28 = -n^2^-1 mod 2^28
    *   off_n2_one28  R28 mod n^2, R28 = 2^(28 L28)
    *   off_table28   table_rows x table_cols entries of L28 limbs, entry [i][j] =
-   *                 hs^((j+1) 2^(group_size i)) R28 mod n^2; -1 when absent (other families, or a
+   *                 hs^((j+1) 2^(W i)) R28 mod n^2; -1 when absent (other families, or a
    *                 table too large to hold twice), and the 32-bit table serves; the powm and
    *                 matmul kernels of that family then also run in 32-bit limbs. */
   int32_t n2_28_len, table28_log2g;
   uint32_t n2_minv28;
   int64_t off_n2_28, off_n2_one28, off_table28;
   int64_t off_n2_r2_28;   /* R28^2 mod n^2 (same L28): powm and matmul of that family in radix 2^28 */
+  /* Width W of the fixed-base table's windows (both layouts): table_rows = ceil(a_bits / W),
+   * table_cols = 2^W - 1, entry [i][j] = hs^((j+1) 2^(W i)). The kernels bit-reverse a's
+   * group_size-bit groups first (a -> a', as mpz_fbpowm's index order does) and then take a' in
+   * plain W-bit windows, so W is the build's choice and does not change any result; 0 = W is
+   * group_size (the reference's own table, gmp_utils.cc:56-89). */
+  int32_t table_window;
 } efl_pl_key;
 
 /*
@@ -214,8 +221,9 @@ int efl_pl_add(const void* key_block, const efl_pl_key* key, const uint32_t* x, 
 int efl_pl_powm(const void* key_block, const efl_pl_key* key, const uint32_t* x, const uint32_t* exps,
                 int exp_words, uint32_t* z, int64_t n, void* stream);
 
-/* PaillierInvert (paillier.cc:267-285, :721-797): z = x^-1 mod n^2 (binary extended Euclid on the
- * GPU). bad <- -1, or the first index without an inverse (its z is 0). */
+/* PaillierInvert (paillier.cc:267-285, :721-797): z = x^-1 mod n^2 (Pornin's batched binary GCD,
+ * "Optimized Binary GCD for Modular Inversion", 2020, on the GPU). bad <- -1, or
+ * the first index without an inverse (its z is 0). */
 int efl_pl_invert(const void* key_block, const efl_pl_key* key, const uint32_t* x, uint32_t* z,
                   int64_t n, int64_t* bad, void* stream);
 

@@ -132,3 +132,14 @@ def test_product_does_not_import_oracle():
             if f.endswith(".py"):
                 src = open(os.path.join(dirpath, f)).read()
                 assert "oracle" not in re.findall(r"^\s*(?:from|import)\s+(\w+)", src, re.M), f
+
+
+def test_table_window_choice():
+    """choose_table_window: the widest window whose table fits 2^18 entries."""
+    from efl.privacy.paillier_cipher import choose_table_window, TABLE_MAX_ENTRIES
+    assert choose_table_window(2048) == 10        # reference default key: 4096-bit n, 2048-bit a
+    assert choose_table_window(512) == 12         # the examples' 1024-bit key
+    for a_bits in (1, 7, 64, 256, 513, 1024, 2048, 4096, 8192):
+        W = choose_table_window(a_bits)
+        assert -(-a_bits // W) * ((1 << W) - 1) <= TABLE_MAX_ENTRIES
+        assert W == 16 or -(-a_bits // (W + 1)) * ((1 << (W + 1)) - 1) > TABLE_MAX_ENTRIES

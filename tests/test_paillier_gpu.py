@@ -90,6 +90,54 @@ def test_fbpowm_kat(efl, k, c):
         assert out.to_hex().strings() == [v["hsa"] for v in vs]
 
 
+@pytest.mark.parametrize("W", [1, 3, 7, 12])
+@pytest.mark.parametrize("k,c", fams(ENC_KEYS))
+def test_fbpowm_kat_any_table_window(efl, k, c, W):
+    """The table's own window W is a build choice: the kernels reverse a's API-group bits
+    (a -> a', as mpz_fbpowm's lookup does) and walk a' in W-bit windows. Every (g, W) pair gives
+    the reference's hs^(a') bit for bit, and so does fresh-randomness encryption."""
+    for g in sorted({v["g"] for v in k["vectors"]}):
+        kp = efl.paillier.Keypair(seed=77)
+        kp.set_keys_ints(int(k["n"], 16), int(k["hs"], 16), k["a_bits"] // 8, g, table_window=W)
+        assert kp.key.desc.table_window == W and kp.key.desc.table_cols == (1 << W) - 1
+        vs = [v for v in k["vectors"] if v["g"] == g]
+        with family(k["n_bytes"] // 4, False, c):
+            out = kp.fbpowm(a=[int(v["a"], 16) for v in vs])
+            ct = kp.encrypt(torch.tensor([3, -5]), counter_base=40)
+        assert out.to_hex().strings() == [v["hsa"] for v in vs]
+        okp = P.Keypair(int(k["n"], 16), int(k["hs"], 16), k["a_bits"] // 8, g)
+        want = [P.hx(P.encrypt(okp, m, P.fbpowm(okp.hs, okp.n2, philox.draw_a(77, 40 + i, k["a_bits"]), g)))
+                for i, m in enumerate([3, -5])]
+        assert ct.tensor.to_hex().strings() == want
+
+
+def test_table_built_on_gpu_matches_host(efl):
+    """The fixed-base table efl builds on the GPU (row bases on the host, entries base^j by
+    efl_pl_powm, then x R and x R28 by efl_pl_add) equals hs^(j 2^(W i)) R mod n^2 computed with
+    Python ints, in both layouts."""
+    from efl.privacy import paillier_cipher as pc
+    k = ENC_KEYS[1]
+    n, hs = int(k["n"], 16), int(k["hs"], 16)
+    kb = pc.KeyBlock(n, hs, k["a_bits"], 1, table_window=5)
+    d = kb.desc
+    n2 = n * n
+    R = 1 << (32 * kb.lc)
+    blk = kb.block.cpu().numpy().view(np.uint32)
+    rng = np.random.default_rng(2)
+    for _ in range(40):
+        i, j = int(rng.integers(0, d.table_rows)), int(rng.integers(1, d.table_cols + 1))
+        want = pow(hs, j << (5 * i), n2)
+        off = d.off_table + (i * d.table_cols + j - 1) * kb.lc
+        got = int.from_bytes(blk[off:off + kb.lc].tobytes(), "little")
+        assert got == want * R % n2, (i, j)
+        if d.off_table28 >= 0:
+            L28 = d.n2_28_len
+            off = d.off_table28 + (i * d.table_cols + j - 1) * L28
+            limbs = blk[off:off + L28]
+            got28 = sum(int(v) << (28 * t) for t, v in enumerate(limbs))
+            assert got28 == want * (1 << (28 * L28)) % n2, (i, j)
+
+
 @pytest.mark.parametrize("k,c", fams(ALL))
 def test_homomorphic_ops_kat(efl, k, c):
     kp = keypair(efl, k)

@@ -95,3 +95,78 @@ def test_paillier_layer_two_party(kind):
     assert torch.allclose(dW + dws, want_dw, rtol=1e-2, atol=1e-2)
     assert (dW - want_dw).abs().mean() > 1.0          # the receiver's share really is masked
     assert torch.allclose(dx, want_dx, rtol=1e-2, atol=1e-2)
+
+
+def party_two_steps(role, my, peer, q):
+    """the receiver's dense with its own plaintext features, two training steps. The
+    functional form must find its layers again on the second call (weights persist and train)."""
+    try:
+        import efl
+        from efl.privacy import paillier_layer as pl
+        Role = efl.privacy.Role
+        units, x, dy_r, dy_s = data("dense")
+        xr = torch.randn(B, 4, generator=torch.Generator().manual_seed(9))
+        c = efl.Communicator(role, 0, 1, f"127.0.0.1:{peer}", f"127.0.0.1:{my}",
+                             default_timeout_milliseconds=120000, connect_retry_seconds=0.1)
+        c.initialize()
+        kp = efl.paillier.Keypair()
+        res = []
+        if role == "follower":
+            efl.paillier.Hook(kp, c, Role.SENDER, "k", n_bytes=64).after_create_session()
+            for _ in range(2):
+                xi = x.cuda().requires_grad_(True)
+                out, w = efl.paillier.sender.dense(xi, kp, c, "l1", units, seed=1)
+                out.backward(dy_s.cuda())
+                c.add_step()
+        else:
+            efl.paillier.Hook(kp, c, Role.RECEIVER, "k", n_bytes=64).after_create_session()
+            lins = []
+            for _ in range(2):
+                y, w = efl.paillier.recver.dense(xr.cuda(), kp, c, "l1", (B, F), units, seed=2)
+                y.backward(dy_r.cuda())
+                lin = pl.cached_layers(c)[("recver.dense.plain", "l1", None)]
+                lins.append(lin)
+                res.append((y.detach(), w.detach(), lin.weight.detach().clone(), lin.bias.detach().clone()))
+                with torch.no_grad():           # one SGD step on the plaintext Dense only
+                    for p in lin.parameters():
+                        p -= 0.5 * p.grad
+                        p.grad = None
+                c.add_step()
+            assert lins[0] is lins[1]
+            assert len(pl.cached_layers(c)) == 2
+        c.shutdown()
+        q.put((role, [tuple(t.cpu().numpy() for t in r) for r in res], None))
+    except BaseException as e:  # pragma: no cover - reported to the parent
+        q.put((role, None, repr(e)))
+
+
+def test_recver_dense_with_inputs_two_steps():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pl, pf = free_port(), free_port()
+    procs = [ctx.Process(target=party_two_steps, args=("leader", pl, pf, q)),
+             ctx.Process(target=party_two_steps, args=("follower", pf, pl, q))]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in procs:
+            role, res, err = q.get(timeout=400)
+            assert err is None, (role, err)
+            results[role] = res
+    finally:
+        for p in procs:
+            p.join(30)
+            if p.is_alive():
+                p.kill()
+    units, x, dy_r, _ = data("dense")
+    xr = torch.randn(B, 4, generator=torch.Generator().manual_seed(9))
+    steps = [tuple(torch.from_numpy(a) for a in r) for r in results["leader"]]
+    for y, W, Wl, bl in steps:
+        assert torch.allclose(y, x @ W + xr @ Wl.t() + bl, rtol=1e-2, atol=1e-2)
+    (_, W0, Wl0, b0), (_, W1, Wl1, b1) = steps
+    assert torch.equal(W0, W1)                       # the Paillier kernel is the same parameter
+    # the SGD step after step 1 is what step 2's plaintext Dense used
+    g_w = dy_r.t() @ xr
+    assert torch.allclose(Wl1, Wl0 - 0.5 * g_w, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(b1, b0 - 0.5 * dy_r.sum(0), rtol=1e-4, atol=1e-5)
