@@ -769,51 +769,79 @@ __global__ __launch_bounds__(256) void k_hex_len(const uint32_t* __restrict__ li
   lens[i] = digits + ((neg && neg[i] && !zero) ? 1 : 0);
 }
 
+// One wave per element for the text itself: a ciphertext's text is hundreds to thousands of
+// characters (512 at 1024-bit n), so one lane per element made every byte access a 64-way
+// scatter (lanes one text apart). Here the 64 lanes of a wave walk ONE text together, lane c on
+// characters c, c + 64, ...: every byte load / store instruction covers 64 consecutive bytes, and
+// the limb words the lanes need are 8 consecutive words (broadcast within groups of 8 lanes).
+constexpr int kHexWaves = 4;   // waves (elements) per 256-lane workgroup
+
+__device__ __forceinline__ char hex_char(uint32_t v) { return (char)(v < 10 ? '0' + v : 'a' + v - 10); }
+
+// value of a hex digit, or 16 for anything else
+__device__ __forceinline__ uint32_t hex_val(char c) {
+  if (c >= '0' && c <= '9') return (uint32_t)(c - '0');
+  if (c >= 'a' && c <= 'f') return (uint32_t)(c - 'a' + 10);
+  if (c >= 'A' && c <= 'F') return (uint32_t)(c - 'A' + 10);
+  return 16u;
+}
+
 __global__ __launch_bounds__(256) void k_hex_write(const uint32_t* __restrict__ limbs, int L,
                                                    const signed char* __restrict__ neg,
                                                    const long long* __restrict__ offs,
                                                    char* __restrict__ chars, long long N) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long i = (long long)blockIdx.x * kHexWaves + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (i >= N) return;
   const uint32_t* x = limbs + i * L;
-  char* o = chars + offs[i];
-  long long len = offs[i + 1] - offs[i];
-  long long pos = 0;
-  int digits = (int)len;
-  if (len > 1 && neg && neg[i]) { o[pos++] = '-'; digits -= 1; }
-  for (int d = digits - 1; d >= 0; --d) {
-    const uint32_t v = (x[d >> 3] >> ((d & 7) * 4)) & 15u;
-    o[pos++] = (char)(v < 10 ? '0' + v : 'a' + v - 10);
+  const long long o0 = offs[i], len = offs[i + 1] - o0;
+  const bool sign = len > 1 && neg && neg[i];
+  if (sign && lane == 0) chars[o0] = '-';
+  char* o = chars + o0 + (sign ? 1 : 0);
+  const long long digits = len - (sign ? 1 : 0);
+  for (long long c = lane; c < digits; c += 64) {
+    const long long d = digits - 1 - c;   // digit index from the least significant
+    o[c] = hex_char((x[d >> 3] >> ((d & 7) * 4)) & 15u);
   }
 }
 
-// parse [-]hexdigits into L limbs; bad <- smallest index of a malformed / too-wide string
+// parse [-]hexdigits into L limbs; bad <- smallest index of a malformed / too-wide string.
+// Lane w assembles limbs w, w + 64, ... from their 8 digits; digits past 8 L must be '0'.
 __global__ __launch_bounds__(256) void k_hex_parse(const char* __restrict__ chars,
                                                    const long long* __restrict__ offs, int L,
                                                    uint32_t* __restrict__ limbs,
                                                    signed char* __restrict__ neg, long long N,
                                                    unsigned long long* bad) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long i = (long long)blockIdx.x * kHexWaves + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (i >= N) return;
   long long s = offs[i];
   const long long e = offs[i + 1];
-  uint32_t* x = limbs + i * L;
-  for (int w = 0; w < L; ++w) x[w] = 0;
-  bool ok = e > s, ng = false;
-  if (ok && chars[s] == '-') { ng = true; ++s; ok = e > s; }
-  while (ok && s < e - 1 && chars[s] == '0') ++s;
-  if (ok && e - s > 8LL * L) ok = false;
-  for (long long j = e - 1, d = 0; ok && j >= s; --j, ++d) {
-    const char c = chars[j];
-    uint32_t v;
-    if (c >= '0' && c <= '9') v = c - '0';
-    else if (c >= 'a' && c <= 'f') v = c - 'a' + 10;
-    else if (c >= 'A' && c <= 'F') v = c - 'A' + 10;
-    else { ok = false; break; }
-    x[d >> 3] |= v << ((d & 7) * 4);
+  bool ok = e > s;
+  const bool ng = ok && chars[s] == '-';
+  if (ng) {
+    ++s;
+    ok = e > s;
   }
-  if (neg) neg[i] = ng ? 1 : 0;
-  if (!ok) atomicMin(bad, (unsigned long long)i);
+  const long long nd = ok ? e - s : 0;
+  uint32_t* x = limbs + i * L;
+  for (int w = lane; w < L; w += 64) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const long long d = 8ll * w + t;
+      if (d < nd) {
+        const uint32_t v = hex_val(chars[e - 1 - d]);
+        ok = ok && v < 16u;
+        acc |= (v & 15u) << (4 * t);
+      }
+    }
+    x[w] = acc;
+  }
+  for (long long d = 8ll * L + lane; d < nd; d += 64) ok = ok && chars[e - 1 - d] == '0';
+  if (neg && lane == 0) neg[i] = ng ? 1 : 0;
+  // one report per element: any lane that saw a bad character
+  if (__any(!ok) && lane == 0) atomicMin(bad, (unsigned long long)i);
 }
 
 // decrypt -> int64 (mpz_get_sll semantics, gmp_utils.cc:38-45: low 64 bits of |m|, then sign)
@@ -1109,7 +1137,7 @@ EFL_API int efl_hex_lengths(const uint32_t* limbs, int limbs_per_elem, const int
 EFL_API int efl_hex_write(const uint32_t* limbs, int limbs_per_elem, const int8_t* negative,
                           const int64_t* offsets, char* chars, int64_t n, void* stream) {
   if (n <= 0) return n < 0 ? EFL_E_INVALID_ARGUMENT : EFL_OK;
-  hipLaunchKernelGGL(k_hex_write, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, limbs,
+  hipLaunchKernelGGL(k_hex_write, dim3((unsigned)((n + kHexWaves - 1) / kHexWaves)), dim3(256), 0, (hipStream_t)stream, limbs,
                      limbs_per_elem, (const signed char*)negative, (const long long*)offsets, chars, (long long)n);
   return hip_status(hipGetLastError(), "efl_hex_write");
 }
@@ -1120,7 +1148,7 @@ EFL_API int efl_hex_parse(const char* chars, const int64_t* offsets, int limbs_p
   hipStream_t s = (hipStream_t)stream;
   hipError_t e = hipMemsetAsync(bad, 0xFF, sizeof(int64_t), s);
   if (e != hipSuccess || n <= 0) return hip_status(e, "efl_hex_parse");
-  hipLaunchKernelGGL(k_hex_parse, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, chars,
+  hipLaunchKernelGGL(k_hex_parse, dim3((unsigned)((n + kHexWaves - 1) / kHexWaves)), dim3(256), 0, s, chars,
                      (const long long*)offsets, limbs_per_elem, limbs, (signed char*)negative, (long long)n,
                      (unsigned long long*)bad);
   return hip_status(hipGetLastError(), "efl_hex_parse");

@@ -20,6 +20,9 @@ run() {
     pl)     timeout -k 10 600 python -u -m pytest tests/test_paillier_gpu.py tests/test_distributed_gpu.py -m gpu -x -q \
               --timeout 300 --timeout-method thread > gpurun_out/pytest_pl.log 2>&1 ;;
     stagep) timeout -k 10 900 python -u bench.py --stage p --no-cpu-baseline > gpurun_out/stage_p.jsonl 2> gpurun_out/stage_p.err ;;
+    hex)    timeout -k 10 240 python -u tools/bench_hex.py > gpurun_out/bench_hex.json 2> gpurun_out/bench_hex.err ;;
+    hexprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/hexprof -o run -- \
+              python3 tools/bench_hex.py > gpurun_out/bench_hex_prof.json 2> gpurun_out/hexprof.err ;;
     prof)   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- \
               python3 bench.py --no-extras --no-cpu-baseline > gpurun_out/bench_prof.json 2> gpurun_out/prof.err ;;
     *) echo "unknown step $1"; return 2 ;;
