@@ -23,8 +23,13 @@ run() {
     hex)    timeout -k 10 240 python -u tools/bench_hex.py > gpurun_out/bench_hex.json 2> gpurun_out/bench_hex.err ;;
     hexprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/hexprof -o run -- \
               python3 tools/bench_hex.py > gpurun_out/bench_hex_prof.json 2> gpurun_out/hexprof.err ;;
-    prof)   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- \
-              python3 bench.py --no-extras --no-cpu-baseline > gpurun_out/bench_prof.json 2> gpurun_out/prof.err ;;
+    prof)   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace -o run --output-format csv \
+              -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-extras > gpurun_out/prof_trace.log 2>&1 ;;
+    pmc)    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_fetch -o run --output-format csv \
+              -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-extras > gpurun_out/prof_fetch.log 2>&1 && \
+            timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_write -o run --output-format csv \
+              -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-extras > gpurun_out/prof_write.log 2>&1 ;;
+    smoke)  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
     *) echo "unknown step $1"; return 2 ;;
   esac
 }
