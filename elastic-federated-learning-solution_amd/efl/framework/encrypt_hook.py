@@ -5,9 +5,16 @@ activation, encrypts the mantissa and sends two tensors, '<p>_[x]_mantissa' and 
 the receiving side recv()s both (paillier_layer.py:121, 188). FixedPointHook packages the Stage-F
 part of that pattern as a Communicator hook so existing send/recv callers need no change:
 
-  send(name, float_tensor)  ->  H2D (if host) -> ConvertToFixedPoint on GPU -> D2H into pinned
-                                 buffers -> send(name+'_mantissa', int64) + send(name+'_exponent', int64)
-  recv(name, dtype=float)   ->  recv both -> H2D -> FixedPointToFloatPoint on GPU -> tensor
+  send(name, float_tensor)  ->  ConvertToFixedPoint on GPU -> pinned host M, E ->
+                                 send(name+'_mantissa', int64) + send(name+'_exponent', int64)
+  recv(name, dtype=float)   ->  recv both -> FixedPointToFloatPoint on GPU -> tensor
+
+Host tensors (the reference's case: its ops run on the CPU and the communicator ships host
+buffers) go through efl.framework.host_pipeline.PinnedCodecPipeline: chunked H2D | codec | D2H on
+three streams, so each leg runs at the rate of its slower PCIe direction; a pageable source (the
+bytes gRPC hands over on receive) is staged through pinned chunk buffers inside the pipeline.
+A device tensor is encoded where it is and copied out once; recv with return_device="cuda"
+decodes on the device.
 
 The codec functions are injectable (`encode=`, `decode=`) so CPU-only tests can run the same
 plumbing with a CPU checker; by default they are the libefl_hip.so ops (no CPU fallback).
@@ -32,6 +39,7 @@ class _PinnedPool:
         self._bufs = {}
 
     def get(self, like: torch.Tensor, slot: str) -> torch.Tensor:
+        """A pinned buffer of like's dtype and shape (`like` may be a meta tensor)."""
         k = (slot, like.dtype, like.numel())
         b = self._bufs.get(k)
         if b is None:
@@ -53,12 +61,21 @@ class FixedPointHook(TensorHook):
         self._names = re.compile(names) if names else None
         self._dp = decrease_precision
         self._return_device = return_device
+        # the pinned three-stream pipeline serves host tensors when the codec is the GPU one
+        self._use_pipeline = encode is None and decode is None
+        self._pipe = None
         if encode is None or decode is None:
             from efl.lib import ops
             encode = encode or ops.convert_to_fixed_point
             decode = decode or ops.fixed_point_to_float_point
         self._encode, self._decode = encode, decode
         self._pool = _PinnedPool() if reuse_buffers else None
+
+    def _pipeline(self):
+        if self._pipe is None:
+            from efl.framework.host_pipeline import PinnedCodecPipeline
+            self._pipe = PinnedCodecPipeline()
+        return self._pipe
 
     def _match(self, name):
         return self._names is None or self._names.search(name) is not None
@@ -73,10 +90,23 @@ class FixedPointHook(TensorHook):
         h.copy_(t, non_blocking=True)
         return h
 
+    def _pinned_like(self, shape, dtype, slot):
+        """Output buffers of a pipeline leg: from the pool (reuse_buffers) or fresh pinned."""
+        if self._pool is not None:
+            return self._pool.get(torch.empty(shape, dtype=dtype, device="meta"), slot)
+        return torch.empty(shape, dtype=dtype, pin_memory=True)
+
     def pre_send(self, name, tensor):
         if not isinstance(tensor, torch.Tensor) or tensor.dtype not in _FLOATS or not self._match(name):
             return None
         t = self._tick()
+        if self._use_pipeline and not tensor.is_cuda:
+            # host tensor: H2D | encode | D2H pipelined into pinned M, E (the gRPC payloads)
+            out = (self._pinned_like(tensor.shape, torch.int64, name + "_m"),
+                   self._pinned_like(tensor.shape, torch.int64, name + "_e"))
+            M, E = self._pipeline().encode(tensor, decrease_precision=self._dp, out=out)
+            self._tick("send_pipeline", t)
+            return [(name + "_mantissa", M), (name + "_exponent", E)]
         if self.stats is not None and not tensor.is_cuda and torch.cuda.is_available():
             tensor = tensor.cuda(non_blocking=tensor.is_pinned())
             t = self._tick("send_h2d", t)
@@ -107,6 +137,11 @@ class FixedPointHook(TensorHook):
         M = raw_recv(name + "_mantissa")
         E = raw_recv(name + "_exponent")
         t = self._tick("recv_grpc", t)
+        if self._use_pipeline and self._return_device is None and not M.is_cuda and not E.is_cuda:
+            # host result (the reference's recv): staged H2D | decode | D2H into a pinned tensor
+            y = self._pipeline().decode(M, E, dt, out=self._pinned_like(tuple(M.shape), dt, name + "_y"))
+            self._tick("recv_pipeline", t)
+            return y.reshape(tuple(int(s) for s in shape)) if shape is not None else y
         if torch.cuda.is_available():
             M = M.cuda() if not M.is_cuda else M
             E = E.cuda() if not E.is_cuda else E

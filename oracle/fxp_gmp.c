@@ -201,3 +201,87 @@ EFL_EXPORT void baseline_decode_f32_mt(const int64_t* M, const int64_t* E, float
   j.Mi = M; j.Ei = E; j.y = y; j.mode = 1; j.ftz = ftz;
   run_sharded(j, n, nthreads);
 }
+
+/* ------------------------- exhaustive fp32 check (tools/exhaustive_fxp.py) ------------------- */
+
+/* Position-weighted sums mod 2^64 over fp32 bit patterns start .. start+count-1 (uint32 wrap) of
+ *   h[0] = sum (M K1 + E K2) (2 i + 1)      the literal encode loop (fixed_point.cc:107-137)
+ *   h[1] = sum y0 K3 (2 i + 1)               y0 = GMP decode of (M, E), MXCSR default
+ *   h[2] = sum y1 K3 (2 i + 1)               y1 = the same under FTZ|DAZ (TF threadpool state)
+ * i = the global pattern index (start + offset), y = float bits. Sums mod 2^64 do not depend on the
+ * order of the additions, so the GPU side (torch int64 arithmetic) reproduces them exactly. */
+#define EH_K1 0x9E3779B97F4A7C15ull
+#define EH_K2 0xC2B2AE3D27D4EB4Full
+#define EH_K3 0x165667B19E3779F9ull
+
+typedef struct {
+  uint32_t start;
+  int64_t s, e;
+  int dp;
+  uint64_t h[3];
+} eh_job_t;
+
+static void* eh_worker(void* p) {
+  eh_job_t* j = (eh_job_t*)p;
+  enum { B = 4096 };
+  float x[B];
+  int64_t M[B], E[B];
+  mpf_t op;
+  mpz_t z;
+  mpf_init(op);
+  mpz_init(z);
+  uint64_t h0 = 0, h1 = 0, h2 = 0;
+  for (int64_t b0 = j->s; b0 < j->e; b0 += B) {
+    const int64_t nb = j->e - b0 < B ? j->e - b0 : B;
+    for (int64_t k = 0; k < nb; ++k) {
+      const uint32_t bits = j->start + (uint32_t)(b0 + k);
+      memcpy(&x[k], &bits, 4);
+    }
+    encode_f32_literal(x, M, E, 0, nb, j->dp);
+    for (int mode = 0; mode < 2; ++mode) {
+      const unsigned old = set_ftz(mode);
+      uint64_t acc = 0;
+      for (int64_t k = 0; k < nb; ++k) {
+        set_sll(z, M[k]);
+        mpf_set_z(op, z);
+        scale_2exp(op, E[k]);
+        const float y = (float)mpf_get_d(op);
+        uint32_t yb;
+        memcpy(&yb, &y, 4);
+        const uint64_t w = 2 * ((uint64_t)j->start + (uint64_t)(b0 + k)) + 1;
+        acc += (uint64_t)yb * EH_K3 * w;
+        if (mode == 0) h0 += ((uint64_t)M[k] * EH_K1 + (uint64_t)E[k] * EH_K2) * w;
+      }
+      _mm_setcsr(old);
+      if (mode == 0) h1 += acc;
+      else h2 += acc;
+    }
+  }
+  mpz_clear(z);
+  mpf_clear(op);
+  j->h[0] = h0;
+  j->h[1] = h1;
+  j->h[2] = h2;
+  return NULL;
+}
+
+EFL_EXPORT void exhaustive_hash_f32(uint32_t start, int64_t count, int dp, int nthreads, uint64_t* out) {
+  if (nthreads < 1) nthreads = 1;
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nthreads);
+  eh_job_t* jobs = (eh_job_t*)malloc(sizeof(eh_job_t) * (size_t)nthreads);
+  const int64_t blk = (count + nthreads - 1) / nthreads;
+  for (int t = 0; t < nthreads; ++t) {
+    jobs[t].start = start;
+    jobs[t].dp = dp;
+    jobs[t].s = t * blk < count ? t * blk : count;
+    jobs[t].e = (t + 1) * blk < count ? (t + 1) * blk : count;
+    pthread_create(&th[t], NULL, eh_worker, &jobs[t]);
+  }
+  out[0] = out[1] = out[2] = 0;
+  for (int t = 0; t < nthreads; ++t) {
+    pthread_join(th[t], NULL);
+    for (int k = 0; k < 3; ++k) out[k] += jobs[t].h[k];
+  }
+  free(th);
+  free(jobs);
+}

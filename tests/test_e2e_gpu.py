@@ -1,0 +1,80 @@
+"""GPU, two processes: BASELINE config 5 in small — the two-party loopback end to end with the real
+codec on each side, as a deployment runs it (one process per party, here sharing the box's GPU):
+
+  follower: host fp32 -> FixedPointHook (pinned H2D | encode | D2H pipeline) -> gRPC M + E
+  leader:   gRPC -> FixedPointHook (staged H2D | decode | D2H pipeline) -> host fp32
+
+The decoded tensor must equal the sent one bit for bit (FTZ decode: +-0 round-trips to +-0), for a
+pinned and a pageable source, over two steps with reused pinned buffers."""
+import multiprocessing as mp
+
+import numpy as np
+import pytest
+import torch
+
+from test_communicator import free_port
+
+pytestmark = pytest.mark.gpu
+
+SHAPE = (2048, 1000)          # 7.8 MiB fp32; 2 pipeline chunks of 4 Mi elements (ragged)
+
+
+def _x(step):
+    x = torch.randn(*SHAPE, generator=torch.Generator().manual_seed(100 + step))
+    x[0, :4] = torch.tensor([0.0, -0.0, 8388608.0, -1.5e-40])
+    x[1] = torch.relu(x[1])
+    return x
+
+
+def party(role, my, peer, q):
+    try:
+        import efl
+        stats = {}
+        hook = efl.privacy.FixedPointHook(reuse_buffers=True, stats=stats)
+        c = efl.Communicator(role, 0, 1, f"127.0.0.1:{peer}", f"127.0.0.1:{my}", hooks=[hook],
+                             default_timeout_milliseconds=120000, connect_retry_seconds=0.1)
+        c.initialize()
+        got = []
+        for step in range(2):
+            if role == "follower":
+                x = _x(step)
+                c.send("act_[x]", x.pin_memory() if step == 0 else x).result()
+            else:
+                y = c.recv("act_[x]", shape=SHAPE)
+                got.append((y.is_pinned(), y.numpy().view(np.uint32).copy()))
+            c.add_step()
+        c.shutdown()
+        q.put((role, got, sorted(stats), None))
+    except BaseException as e:  # pragma: no cover - reported to the parent
+        q.put((role, None, None, repr(e)))
+
+
+def test_two_process_loopback_pipelined_hook():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pl, pf = free_port(), free_port()
+    procs = [ctx.Process(target=party, args=("leader", pl, pf, q)),
+             ctx.Process(target=party, args=("follower", pf, pl, q))]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in procs:
+            role, got, stages, err = q.get(timeout=110)
+            assert err is None, (role, err)
+            res[role] = (got, stages)
+    finally:
+        for p in procs:
+            p.join(30)
+            if p.is_alive():
+                p.kill()
+    got, stages = res["leader"]
+    assert "recv_pipeline" in stages and "send_pipeline" in res["follower"][1]
+    for step, (pinned, ybits) in enumerate(got):
+        assert pinned
+        x = _x(step)
+        want = x.numpy().view(np.uint32).copy()
+        # FTZ decode: denormal inputs come back as signed zero, everything else exactly
+        den = (np.abs(x.numpy()) < np.float32(1.1754944e-38)) & (x.numpy() != 0)
+        want[den] &= 0x80000000
+        assert np.array_equal(ybits, want), step

@@ -326,3 +326,32 @@ def test_full_size_properties(efl):
     # checksum of the whole output against an oracle pass over the whole tensor
     Mo_all, Eo_all = fxp.encode(host(x))
     assert int(M.sum()) == int(Mo_all.sum()) and int(E.sum()) == int(Eo_all.sum())
+
+
+# ------------------------------------------------- slices of the exhaustive fp32 sweep
+# tools/exhaustive_fxp.py runs all 2^32 patterns (profiles/r02/exhaustive_fp32.json); here the
+# same check on 2^20-pattern slices at the boundaries: +0 and the denormals, the |x| in [2^23, 2^24)
+# band that loses its implicit bit, inf / NaN, and the negative mirror of each.
+
+@pytest.mark.parametrize("start", [0x00000000, 0x007F0000, 0x4AF80000, 0x4B7F0000, 0x7F780000, 0x7FF00000,
+                                   0x80000000, 0xCAF80000, 0xFF780000])
+@pytest.mark.parametrize("dp", [0, 1])
+def test_exhaustive_slice_vs_literal_loop_and_gmp(efl, start, dp):
+    from tools import exhaustive_fxp as ex
+    dev = efl.lib.require_gpu()
+    count = 1 << 20
+    assert ex.gpu_hash(efl, start, count, dp, dev) == ex.cpu_hash(start, count, dp, 8)
+
+
+def test_exhaustive_all_fp32_patterns(efl):
+    """Every one of the 2^32 fp32 bit patterns, both decrease_precision values, decode in both
+    MXCSR modes: the GPU kernels equal the reference loop (restated statement for statement) + GMP
+    (tools/exhaustive_fxp.py; ~15 s on the GPU box's 16 host threads)."""
+    from tools import exhaustive_fxp as ex
+    import bench
+    dev = efl.lib.require_gpu()
+    threads = bench.usable_cores()[0]
+    chunk = 1 << 26
+    for dp in (0, 1):
+        for start in range(0, 1 << 32, chunk):
+            assert ex.gpu_hash(efl, start, chunk, dp, dev) == ex.cpu_hash(start, chunk, dp, threads), (dp, hex(start))

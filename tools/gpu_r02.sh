@@ -29,6 +29,9 @@ run() {
               -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-extras > gpurun_out/prof_fetch.log 2>&1 && \
             timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_write -o run --output-format csv \
               -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-extras > gpurun_out/prof_write.log 2>&1 ;;
+    exh)    timeout -k 10 900 python -u tools/exhaustive_fxp.py > gpurun_out/exhaustive.json 2> gpurun_out/exhaustive.err ;;
+    fxp)    timeout -k 10 600 python -u -m pytest tests/test_fxp_gpu.py -m gpu -x -q --timeout 120 \
+              --timeout-method thread > gpurun_out/pytest_fxp.log 2>&1 ;;
     smoke)  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
     *) echo "unknown step $1"; return 2 ;;
   esac
