@@ -32,6 +32,9 @@ run() {
     exh)    timeout -k 10 900 python -u tools/exhaustive_fxp.py > gpurun_out/exhaustive.json 2> gpurun_out/exhaustive.err ;;
     fxp)    timeout -k 10 600 python -u -m pytest tests/test_fxp_gpu.py -m gpu -x -q --timeout 120 \
               --timeout-method thread > gpurun_out/pytest_fxp.log 2>&1 ;;
+    e2e)    timeout -k 10 300 python -u -m pytest tests/test_e2e_gpu.py tests/test_hook_gpu.py -m gpu -x -v --timeout 150 \
+              --timeout-method thread > gpurun_out/pytest_e2e.log 2>&1 ;;
+    e2ebench) timeout -k 10 600 python -u tools/bench_e2e.py > gpurun_out/bench_e2e.json 2> gpurun_out/bench_e2e.err ;;
     smoke)  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
     *) echo "unknown step $1"; return 2 ;;
   esac
