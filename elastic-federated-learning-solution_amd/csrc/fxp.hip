@@ -455,6 +455,13 @@ std::atomic<int> g_grid_cap{0};   // 0: one tile per workgroup; else max workgro
 // 7 loads + `nt sc1` stores (default, as the streaming encode)
 std::atomic<int> g_batch_enc_nt{7};
 constexpr int kEnc = 0, kDec = 1;
+// batched tile (efl_fxp_encode_batched / decode_batched): B lanes x K pairs per workgroup
+constexpr int kBatchB = 256, kBatchK = 4;
+constexpr long long kMaxGridY = 65535;
+// fp32 [encode, decode]: encode 256 x 2 pairs measured 1.5-2 % faster than 256 x 4 in the config-3
+// step (tools/batched_probe.py, profiles/r02/batched_probe*.json); decode's shape is within noise
+std::atomic<int> g_batch_block[2] = {{kBatchB}, {kBatchB}};
+std::atomic<int> g_batch_k[2] = {{2}, {kBatchK}};
 
 template <class Op, int B, int K, int NT>
 hipError_t launch_k(const typename Op::Args& a, long long nunits, hipStream_t s) {
@@ -560,6 +567,15 @@ using namespace efl;
 EFL_API const char* efl_last_error(void) { return t_err.c_str(); }
 
 EFL_API int efl_fxp_tune(int kind, int value) {
+  if (kind >= 10 && kind <= 13) {   // batched fp32: 10/11 encode block/K, 12/13 decode block/K
+    const int dir = kind >= 12 ? kDec : kEnc;
+    if (kind % 2 == 0) {
+      if (value != 256 && value != 512) return EFL_E_INVALID_ARGUMENT;
+      return g_batch_block[dir].exchange(value);
+    }
+    if (value != 1 && value != 2 && value != 4) return EFL_E_INVALID_ARGUMENT;
+    return g_batch_k[dir].exchange(value);
+  }
   if (kind == 9) {
     if (value != 1 && value != 3 && value != 7) return EFL_E_INVALID_ARGUMENT;
     return g_batch_enc_nt.exchange(value);
@@ -663,27 +679,47 @@ EFL_API int efl_fxp_decode_hex(const char* chars, const int64_t* offsets, const 
 }
 
 namespace {
-// batched tile: 256 lanes x 4 pairs (2048 elements), nontemporal loads: fewer, longer workgroups
-// amortise the per-workgroup pointer-table reads (measured faster than the k_stream shape here)
-constexpr int kBatchB = 256, kBatchK = 4;
-constexpr long long kMaxGridY = 65535;
+// batched tile: B lanes x K pairs, nontemporal loads: fewer, longer workgroups amortise the
+// per-workgroup pointer-table reads. Default 256 x 4 (2048 elements, measured faster than the
+// k_stream shape here); the fp32 shapes are tunable (efl_fxp_tune kinds 10-13).
 
-template <class Op, int NT>
-hipError_t launch_batched(const void* const* src, void* const* d0, void* const* d1,
-                          const long long* ns, long long count, long long max_n, int flag,
-                          hipStream_t s) {
-  const long long tile = (long long)kBatchB * kBatchK * Op::kElems;
+template <class Op, int NT, int B, int K>
+hipError_t launch_batched_bk(const void* const* src, void* const* d0, void* const* d1,
+                             const long long* ns, long long count, long long max_n, int flag,
+                             hipStream_t s) {
+  const long long tile = (long long)B * K * Op::kElems;
   const long long gx = (max_n + tile - 1) / tile;
   if (gx == 0 || count == 0) return hipSuccess;
   if (gx > 0x7FFFFFFFll) return hipErrorInvalidValue;
   for (long long b = 0; b < count; b += kMaxGridY) {
     const long long gy = count - b < kMaxGridY ? count - b : kMaxGridY;
-    hipLaunchKernelGGL((k_batched<Op, kBatchB, kBatchK, NT>), dim3((unsigned)gx, (unsigned)gy), dim3(kBatchB), 0, s,
+    hipLaunchKernelGGL((k_batched<Op, B, K, NT>), dim3((unsigned)gx, (unsigned)gy), dim3(B), 0, s,
                        src, d0, d1, ns, flag, b);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
+}
+
+template <class Op, int NT>
+hipError_t launch_batched(const void* const* src, void* const* d0, void* const* d1,
+                          const long long* ns, long long count, long long max_n, int flag,
+                          hipStream_t s) {
+  return launch_batched_bk<Op, NT, kBatchB, kBatchK>(src, d0, d1, ns, count, max_n, flag, s);
+}
+
+// the fp32 ops, at the tuned shape of their direction
+template <class Op, int NT>
+hipError_t launch_batched_f32(int dir, const void* const* src, void* const* d0, void* const* d1,
+                              const long long* ns, long long count, long long max_n, int flag,
+                              hipStream_t s) {
+  const int B = g_batch_block[dir].load(std::memory_order_relaxed);
+  const int K = g_batch_k[dir].load(std::memory_order_relaxed);
+#define EFL_BK(B_, K_) \
+  if (B == B_ && K == K_) return launch_batched_bk<Op, NT, B_, K_>(src, d0, d1, ns, count, max_n, flag, s);
+  EFL_BK(256, 1) EFL_BK(256, 2) EFL_BK(256, 4) EFL_BK(512, 1) EFL_BK(512, 2) EFL_BK(512, 4)
+#undef EFL_BK
+  return launch_batched_bk<Op, NT, kBatchB, kBatchK>(src, d0, d1, ns, count, max_n, flag, s);
 }
 }  // namespace
 
@@ -701,9 +737,9 @@ EFL_API int efl_fxp_encode_batched(const void* const* xs, int dtype, int64_t* co
   switch (dtype) {
     case EFL_DT_FLOAT:
       switch (g_batch_enc_nt.load()) {
-        case 7: e = launch_batched<EncF32Pair, 7>(xs, d0, d1, nn, count, max_n, f, s); break;
-        case 3: e = launch_batched<EncF32Pair, 3>(xs, d0, d1, nn, count, max_n, f, s); break;
-        default: e = launch_batched<EncF32Pair, 1>(xs, d0, d1, nn, count, max_n, f, s); break;
+        case 7: e = launch_batched_f32<EncF32Pair, 7>(kEnc, xs, d0, d1, nn, count, max_n, f, s); break;
+        case 3: e = launch_batched_f32<EncF32Pair, 3>(kEnc, xs, d0, d1, nn, count, max_n, f, s); break;
+        default: e = launch_batched_f32<EncF32Pair, 1>(kEnc, xs, d0, d1, nn, count, max_n, f, s); break;
       }
       break;
     case EFL_DT_DOUBLE: e = launch_batched<EncF64Pair, 1>(xs, d0, d1, nn, count, max_n, f, s); break;
@@ -729,7 +765,7 @@ EFL_API int efl_fxp_decode_batched(const int64_t* const* mantissas, const int64_
   auto nn = (const long long*)ns;
   hipError_t e;
   switch (dtype) {
-    case EFL_DT_FLOAT: e = launch_batched<DecF32Pair, 1>(src, d0, ys, nn, count, max_n, flags, s); break;
+    case EFL_DT_FLOAT: e = launch_batched_f32<DecF32Pair, 1>(kDec, src, d0, ys, nn, count, max_n, flags, s); break;
     case EFL_DT_DOUBLE: e = launch_batched<DecF64Pair, 1>(src, d0, ys, nn, count, max_n, flags, s); break;
     default:
       set_error("FixedPointToFloatPoint: unsupported dtype %d", dtype);

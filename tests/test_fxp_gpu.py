@@ -284,6 +284,25 @@ def test_batched_ragged(efl):
         assert np.array_equal(bits32(y), fxp.decode(Mo, Eo).view(np.uint32))
 
 
+@pytest.mark.parametrize("knob", [(10, 512), (11, 1), (11, 4), (12, 512), (13, 2)])
+def test_batched_tuning_variants_identical(efl, knob):
+    """Every batched fp32 tile shape (efl_fxp_tune 10-13) gives the same bits."""
+    lib = efl.lib.raw()
+    sizes = [1, 5, 4095, 16384, 30001]
+    xs_np = [rand_bits(n, 40 + n).view(np.float32) for n in sizes]
+    prev = lib.efl_fxp_tune(*knob)
+    assert prev > 0
+    try:
+        Ms, Es = efl.lib.ops.convert_to_fixed_point_batched([dev(a) for a in xs_np])
+        ys = efl.lib.ops.fixed_point_to_float_point_batched(Ms, Es)
+    finally:
+        lib.efl_fxp_tune(knob[0], prev)
+    for a, M, E, y in zip(xs_np, Ms, Es, ys):
+        Mo, Eo = fxp.encode(a)
+        assert np.array_equal(host(M), Mo) and np.array_equal(host(E), Eo)
+        assert np.array_equal(bits32(y), fxp.decode(Mo, Eo).view(np.uint32))
+
+
 def test_batched_embedding_slices(efl):
     """BASELINE config 3 shape: 4096 x 64 KiB fp32 slices, N(0, 0.01), seed 1."""
     g = torch.Generator(device="cuda").manual_seed(1)
