@@ -68,8 +68,9 @@ const char* efl_last_error(void);
  * kind = 2*field + direction (direction 0 encode, 1 decode); fields: 0 layout (0 pair, 1 quad),
  * 1 units per lane per tile (1, 2), 2 nontemporal mask (bit0 loads, bit1 stores; 7 = loads plus
  * `nt sc1` 16-B stores, the encode default), 3 workgroup size (128, 256, 512); kind 8 = grid cap
- * (0 = one tile per workgroup); kind 9 = nontemporal mask of the fp32 batched encode (1, 3 or 7).
- * Returns the previous value or EFL_E_INVALID_ARGUMENT. */
+ * (0 = one tile per workgroup); kind 9 = nontemporal mask of the fp32 batched encode (1, 3 or 7);
+ * kinds 10 / 11 = workgroup size (256, 512) / pairs per lane (1, 2, 4) of the fp32 batched encode,
+ * 12 / 13 the same for the batched decode. Returns the previous value or EFL_E_INVALID_ARGUMENT. */
 int efl_fxp_tune(int kind, int value);
 
 /* ----------------------------------------------------------------------------------------- */

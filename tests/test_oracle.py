@@ -155,3 +155,18 @@ def test_baseline_matches_oracle():
 def test_decode_size_mismatch():
     with pytest.raises(ValueError, match="same size"):
         fxp.decode(np.zeros(3, np.int64), np.zeros(4, np.int64))
+
+
+@pytest.mark.parametrize("dp", [0, 1])
+def test_literal_loop_matches_restatement(dp):
+    """The timed baseline runs the reference's loop body statement for statement (float-convert
+    ctz, the 0u - 127 shift; oracle/fxp_gmp.c encode_f32_literal); the restatement every other
+    check uses must equal it: 2^20 random patterns plus a stride through all of fp32."""
+    rng = np.random.default_rng(31 + dp)
+    bits = np.concatenate([rng.integers(0, 2**32, 1 << 20, dtype=np.uint64).astype(np.uint32),
+                           np.arange(0, 2**32, 4093, dtype=np.uint64).astype(np.uint32),
+                           G["f32_bits"]])
+    x = bits.view(np.float32)
+    M1, E1 = fxp.encode(x, dp)
+    M2, E2 = fxp.literal_encode_f32(x, dp)
+    assert np.array_equal(M1, M2) and np.array_equal(E1, E2)
