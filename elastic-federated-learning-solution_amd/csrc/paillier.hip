@@ -892,8 +892,11 @@ inline int table_ok(const efl_pl_key* d) {
 
 // kernel family per key size: 0 = one lane per element (paillier.hip), C = sliced over 2ln/C (n^2
 // ops) or ln/C (decryption) lanes of C limbs (paillier_sliced.hip). [ln 16/32/64/128][n^2 ops, decrypt]
-constexpr int kDefaultSlicing[4][2] = {{16, 8}, {16, 32}, {16, 32}, {8, 32}};   // measured: profiles/r01/bench_pl*.jsonl
-int g_slicing[4][2] = {{16, 8}, {16, 32}, {16, 32}, {8, 32}};
+// measured: decryption profiles/r01/bench_pl*.jsonl; n^2 ops profiles/r02/sweep_pl_family.jsonl — with
+// the round-2 table window, 32 limbs per lane is the fastest encryption at every key size (512-bit
+// 1.7x, 1024-bit 1.06x incl. the MNIST matmul, 2048-bit 1.14x, 4096-bit 1.51x the round-1 choice)
+constexpr int kDefaultSlicing[4][2] = {{32, 8}, {32, 32}, {32, 32}, {32, 32}};
+int g_slicing[4][2] = {{32, 8}, {32, 32}, {32, 32}, {32, 32}};
 inline int ln_index(int ln) { return ln == 16 ? 0 : ln == 32 ? 1 : ln == 64 ? 2 : 3; }
 inline int slicing(int ln, int dec) { return g_slicing[ln_index(ln)][dec]; }
 bool g_slicing_set[4][2] = {};   // set explicitly through efl_pl_tune: used as given for every size

@@ -37,6 +37,7 @@ run() {
     e2ebench) timeout -k 10 600 python -u tools/bench_e2e.py > gpurun_out/bench_e2e.json 2> gpurun_out/bench_e2e.err ;;
     bprobe) timeout -k 10 300 python -u tools/batched_probe.py > gpurun_out/batched_probe.json 2> gpurun_out/batched_probe.err ;;
     stagepc) timeout -k 10 1100 python -u bench.py --stage p > gpurun_out/stage_p_cpu.jsonl 2> gpurun_out/stage_p_cpu.err ;;
+    plfam)  timeout -k 10 600 python -u tools/sweep_pl_family.py > gpurun_out/sweep_pl_family.jsonl 2> gpurun_out/sweep_pl_family.err ;;
     smoke)  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
     *) echo "unknown step $1"; return 2 ;;
   esac
