@@ -151,7 +151,8 @@ struct EncArgs {
   const void* x;
   long long* M;
   long long* E;
-  int flag;   // decrease_precision
+  int flag;       // decrease_precision
+  int e_first;    // fp32 streaming encode: store the exponent pair before the mantissa pair
 };
 struct DecArgs {
   const long long* M;
@@ -169,8 +170,13 @@ struct EncF32Pair {
     long long m0, e0, m1, e1;
     enc_f32(__float_as_uint(v.x), a.flag, m0, e0);
     enc_f32(__float_as_uint(v.y), a.flag, m1, e1);
-    st<NT>((ll2*)a.M + u, ll2{m0, m1});
-    st<NT>((ll2*)a.E + u, ll2{e0, e1});
+    if (a.e_first) {
+      st<NT>((ll2*)a.E + u, ll2{e0, e1});
+      st<NT>((ll2*)a.M + u, ll2{m0, m1});
+    } else {
+      st<NT>((ll2*)a.M + u, ll2{m0, m1});
+      st<NT>((ll2*)a.E + u, ll2{e0, e1});
+    }
   }
   __device__ static void scalar(const Args& a, long long i) {
     long long m, e;
@@ -294,10 +300,14 @@ struct DecF64Pair {
 // Streaming kernel: tiles of B*K units; a workgroup walks tiles blockIdx.x, +gridDim.x, ...
 // Inside a full tile every lane issues its K loads back to back before any store, then transforms
 // and stores. Tile t of a wave touches one contiguous span.
+// xcd_per > 0: XCD-aware tile order. Workgroups are dispatched round-robin over the 8 XCDs
+// (blockIdx % 8); workgroup b then takes tile (b % 8) * xcd_per + b / 8, so each XCD streams one
+// contiguous eighth of the tensor instead of every eighth tile (gridDim.x = 8 * xcd_per).
 template <class Op, int B, int K, int NT>
-__global__ __launch_bounds__(B) void k_stream(typename Op::Args a, long long nunits) {
+__global__ __launch_bounds__(B) void k_stream(typename Op::Args a, long long nunits, int xcd_per) {
   const long long tile = (long long)B * K;
-  for (long long base = (long long)blockIdx.x * tile; base < nunits;
+  const long long t0 = xcd_per > 0 ? (long long)(blockIdx.x & 7u) * xcd_per + (blockIdx.x >> 3) : blockIdx.x;
+  for (long long base = t0 * tile; base < nunits;
        base += (long long)gridDim.x * tile) {
     typename Op::In v[K];
     if (base + tile <= nunits) {
@@ -451,6 +461,10 @@ struct Shape {
 };
 Shape g_shape[2] = {{{0}, {512}, {1}, {7}}, {{0}, {128}, {1}, {1}}};
 std::atomic<int> g_grid_cap{0};   // 0: one tile per workgroup; else max workgroups
+// efl_fxp_tune 14 / 15: XCD-aware tile order (k_stream). Decode on: its kernel 2.3 % and the step
+// 1.2 % faster, encode off: 2.5 % slower (profiles/r02/step_probe_xcd_*.json, same box)
+std::atomic<int> g_xcd_order[2] = {{0}, {1}};
+std::atomic<int> g_e_first{0};                  // efl_fxp_tune 16: encode stores E before M
 // NT mask of the fp32 batched encode (efl_fxp_tune kind 9): 1 nontemporal loads, 3 loads + stores,
 // 7 loads + `nt sc1` stores (default, as the streaming encode)
 std::atomic<int> g_batch_enc_nt{7};
@@ -464,33 +478,39 @@ std::atomic<int> g_batch_block[2] = {{kBatchB}, {kBatchB}};
 std::atomic<int> g_batch_k[2] = {{2}, {kBatchK}};
 
 template <class Op, int B, int K, int NT>
-hipError_t launch_k(const typename Op::Args& a, long long nunits, hipStream_t s) {
+hipError_t launch_k(const typename Op::Args& a, long long nunits, hipStream_t s, int xcd = 0) {
   const long long tile = (long long)B * K;
   long long grid = (nunits + tile - 1) / tile;
   const int cap = g_grid_cap.load(std::memory_order_relaxed);
+  int xcd_per = 0;
   if (cap > 0 && grid > cap) grid = cap;
+  else if (xcd && grid >= 64 && grid < 0x7FFFFFF0ll) {
+    xcd_per = (int)((grid + 7) / 8);
+    grid = 8ll * xcd_per;
+  }
   if (grid > 0x7FFFFFFFll) grid = 0x7FFFFFFFll;
   if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL((k_stream<Op, B, K, NT>), dim3((unsigned)grid), dim3(B), 0, s, a, nunits);
+  hipLaunchKernelGGL((k_stream<Op, B, K, NT>), dim3((unsigned)grid), dim3(B), 0, s, a, nunits, xcd_per);
   return hipGetLastError();
 }
 
 template <class Op, int B, int K>
-hipError_t launch_nt(int nt, const typename Op::Args& a, long long nunits, hipStream_t s) {
+hipError_t launch_nt(int nt, const typename Op::Args& a, long long nunits, hipStream_t s, int xcd) {
   switch (nt) {
-    case 1: return launch_k<Op, B, K, 1>(a, nunits, s);
-    case 2: return launch_k<Op, B, K, 2>(a, nunits, s);
-    case 3: return launch_k<Op, B, K, 3>(a, nunits, s);
-    case 7: return launch_k<Op, B, K, 7>(a, nunits, s);
-    default: return launch_k<Op, B, K, 0>(a, nunits, s);
+    case 1: return launch_k<Op, B, K, 1>(a, nunits, s, xcd);
+    case 2: return launch_k<Op, B, K, 2>(a, nunits, s, xcd);
+    case 3: return launch_k<Op, B, K, 3>(a, nunits, s, xcd);
+    case 7: return launch_k<Op, B, K, 7>(a, nunits, s, xcd);
+    default: return launch_k<Op, B, K, 0>(a, nunits, s, xcd);
   }
 }
 
 template <class Op, int B>
 hipError_t launch_bk(const Shape& sh, const typename Op::Args& a, long long nunits, hipStream_t s) {
   const int nt = sh.nt.load(std::memory_order_relaxed);
-  return sh.k.load(std::memory_order_relaxed) == 2 ? launch_nt<Op, B, 2>(nt, a, nunits, s)
-                                                   : launch_nt<Op, B, 1>(nt, a, nunits, s);
+  const int xcd = g_xcd_order[&sh == &g_shape[kDec] ? kDec : kEnc].load(std::memory_order_relaxed);
+  return sh.k.load(std::memory_order_relaxed) == 2 ? launch_nt<Op, B, 2>(nt, a, nunits, s, xcd)
+                                                   : launch_nt<Op, B, 1>(nt, a, nunits, s, xcd);
 }
 
 // tunable launch (fp32 ops)
@@ -567,6 +587,14 @@ using namespace efl;
 EFL_API const char* efl_last_error(void) { return t_err.c_str(); }
 
 EFL_API int efl_fxp_tune(int kind, int value) {
+  if (kind == 14 || kind == 15) {   // XCD-aware tile order, streaming fp32 encode / decode
+    if (value != 0 && value != 1) return EFL_E_INVALID_ARGUMENT;
+    return g_xcd_order[kind - 14].exchange(value);
+  }
+  if (kind == 16) {                 // streaming fp32 encode: exponent stores first
+    if (value != 0 && value != 1) return EFL_E_INVALID_ARGUMENT;
+    return g_e_first.exchange(value);
+  }
   if (kind >= 10 && kind <= 13) {   // batched fp32: 10/11 encode block/K, 12/13 decode block/K
     const int dir = kind >= 12 ? kDec : kEnc;
     if (kind % 2 == 0) {
@@ -608,7 +636,8 @@ EFL_API int efl_fxp_encode(const void* x, int dtype, int64_t* mantissa, int64_t*
   if (n == 0) return EFL_OK;
   if (!x || !mantissa || !exponent) { set_error("null buffer"); return EFL_E_INVALID_ARGUMENT; }
   hipStream_t s = (hipStream_t)stream;
-  EncArgs a{x, (long long*)mantissa, (long long*)exponent, decrease_precision ? 1 : 0};
+  EncArgs a{x, (long long*)mantissa, (long long*)exponent, decrease_precision ? 1 : 0,
+            g_e_first.load(std::memory_order_relaxed)};
   hipError_t e;
   switch (dtype) {
     case EFL_DT_FLOAT:

@@ -70,7 +70,10 @@ const char* efl_last_error(void);
  * `nt sc1` 16-B stores, the encode default), 3 workgroup size (128, 256, 512); kind 8 = grid cap
  * (0 = one tile per workgroup); kind 9 = nontemporal mask of the fp32 batched encode (1, 3 or 7);
  * kinds 10 / 11 = workgroup size (256, 512) / pairs per lane (1, 2, 4) of the fp32 batched encode,
- * 12 / 13 the same for the batched decode. Returns the previous value or EFL_E_INVALID_ARGUMENT. */
+ * 12 / 13 the same for the batched decode; kinds 14 / 15 = XCD-aware tile order (0 / 1; each of the
+ * 8 XCDs streams one contiguous eighth) of the fp32 streaming encode / decode (default 0 / 1);
+ * kind 16 = the streaming fp32 encode stores the exponent pair before the mantissa pair (0 / 1).
+ * Returns the previous value or EFL_E_INVALID_ARGUMENT. */
 int efl_fxp_tune(int kind, int value);
 
 /* ----------------------------------------------------------------------------------------- */

@@ -250,7 +250,8 @@ def test_errors(efl):
                                                torch.int32)
 
 
-@pytest.mark.parametrize("knob", [(0, 1), (1, 1), (2, 2), (3, 2), (4, 1), (5, 0), (4, 3), (6, 128), (7, 512), (8, 512)])
+@pytest.mark.parametrize("knob", [(0, 1), (1, 1), (2, 2), (3, 2), (4, 1), (5, 0), (4, 3), (6, 128), (7, 512), (8, 512),
+                                  (6, 1024), (14, 1), (15, 0), (16, 1)])
 def test_tuning_variants_identical(efl, knob):
     lib = efl.lib.raw()
     n = (1 << 18) + 7

@@ -33,23 +33,26 @@ y = torch.empty_like(x)
 FLAGS = int(os.environ.get("STEP_DEC_FLAGS", "1"))
 
 # (enc block, enc NT, enc K, dec block, dec NT, dec K, mode)
-DEFAULT = (256, 7, 1, 128, 1, 1)
+DEFAULT = (512, 7, 1, 128, 1, 1)
 ARMS = {"base": DEFAULT + ("loop",), "events": DEFAULT + ("events",), "graph": DEFAULT + ("graph",),
         "dec_nt7": (256, 7, 1, 128, 7, 1, "loop"), "enc_k2": (256, 7, 2, 128, 1, 1, "loop"),
         "enc_b512": (512, 7, 1, 128, 1, 1, "loop")}
 if os.environ.get("STEP_ARMS"):
+    # name:enc_block,enc_nt,enc_k,dec_block,dec_nt,dec_k[,mode[,xcd_enc,xcd_dec,e_first]]
     ARMS = {}
     for a in os.environ["STEP_ARMS"].split(";"):
         name, spec = a.split(":")
         parts = spec.split(",")
-        ARMS[name] = tuple(int(v) for v in parts[:6]) + ((parts[6] if len(parts) > 6 else "loop"),)
+        extra = tuple(int(v) for v in parts[7:10]) if len(parts) > 7 else (0, 0, 0)
+        ARMS[name] = tuple(int(v) for v in parts[:6]) + ((parts[6] if len(parts) > 6 else "loop"),) + extra
 STEPS = int(os.environ.get("STEP_STEPS", "50"))
 ROUNDS = int(os.environ.get("STEP_ROUNDS", "8"))
 
 
 def configure(arm):
     eb, ent, ek, db, dnt, dk = arm[:6]
-    for kind, v in ((6, eb), (4, ent), (2, ek), (7, db), (5, dnt), (3, dk)):
+    xe, xd, ef = arm[7:10] if len(arm) > 7 else (0, 0, 0)
+    for kind, v in ((6, eb), (4, ent), (2, ek), (7, db), (5, dnt), (3, dk), (14, xe), (15, xd), (16, ef)):
         efl.lib.check(min(0, lib.efl_fxp_tune(kind, v)))
 
 
