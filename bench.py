@@ -23,9 +23,10 @@ cpu_baseline: the reference CPU op (oracle/: the literal encode loop of fixed_po
 the GMP mpf decode of :235-248, FTZ|DAZ like a TF threadpool thread, contiguous blocks like TF
 Shard over every usable host core) timed on this box on the same tensor (rank 0, N = 1 only).
 Extra keys at N = 1: "config3" (BASELINE config 3: 4096 x 64 KiB slices, one batched launch per
-direction, and the naive per-slice launches) and "pinned_path" (the north_star's rate including
+direction, and the naive per-slice launches), "pinned_path" (the north_star's rate including
 pinned H2D/D2H copies: efl.framework.host_pipeline over the same tensor, encrypt leg pinned fp32 ->
-pinned M+E, decrypt leg back).
+pinned M+E, decrypt leg back) and "config5" (the two-process gRPC loopback end to end,
+tools/bench_e2e.py, rate including copies).
 
     python bench.py --stage p      Stage P report (SURVEY.md §8(d) last row), one JSON line per key:
 Paillier encrypt (fresh randomness through the fixed-base table) and CRT decrypt of int64
@@ -490,6 +491,23 @@ def stage_p_cpu(n_bytes, a_bytes, g, p, q, hs, threads, cache):
     return cache[key]
 
 
+def config5(timeout_s=240):
+    """BASELINE config 5 (tools/bench_e2e.py): two processes on this box, 256 MiB fp32 from pinned
+    host memory through the pipelined FixedPointHook encode leg, gRPC loopback (2 x 512 MiB messages),
+    the pipelined decode leg, back to host; rate including every copy. Run as a child process so a
+    failure there cannot take the headline line with it (the error is reported instead)."""
+    import subprocess
+    try:
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "bench_e2e.py")], capture_output=True,
+                           text=True, timeout=timeout_s)
+        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        if r.returncode != 0 or not lines:
+            return {"error": f"rc {r.returncode}: {r.stderr.strip()[-300:]}"}
+        return json.loads(lines[-1])
+    except (subprocess.TimeoutExpired, OSError, ValueError) as e:
+        return {"error": repr(e)[:300]}
+
+
 def main():
     args = parse()
     if args.stage == "p":
@@ -626,6 +644,7 @@ def main():
         del M, E, y
         out["config3"] = config3(efl, dev, args.steps)
         out["pinned_path"] = pinned_path(efl, dev, x)
+        out["config5"] = config5()
     if world == 1 and not args.no_cpu_baseline:
         threads, how = (args.cpu_threads, "--cpu-threads") if args.cpu_threads else usable_cores()
         out["cpu_baseline"] = cpu_baseline(x, threads, how, ftz)
