@@ -38,6 +38,10 @@ run() {
     bprobe) timeout -k 10 300 python -u tools/batched_probe.py > gpurun_out/batched_probe.json 2> gpurun_out/batched_probe.err ;;
     stagepc) timeout -k 10 1100 python -u bench.py --stage p > gpurun_out/stage_p_cpu.jsonl 2> gpurun_out/stage_p_cpu.err ;;
     plfam)  timeout -k 10 600 python -u tools/sweep_pl_family.py > gpurun_out/sweep_pl_family.jsonl 2> gpurun_out/sweep_pl_family.err ;;
+    profp)  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_p -o run --output-format csv \
+              -- python3 bench.py --stage p --no-cpu-baseline > gpurun_out/prof_p.log 2>&1 ;;
+    profhex) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_hex -o run --output-format csv \
+              -- python3 tools/bench_hex.py > gpurun_out/prof_hex.log 2>&1 ;;
     smoke)  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
     *) echo "unknown step $1"; return 2 ;;
   esac
