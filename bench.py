@@ -245,6 +245,35 @@ def _mont_macs(L, squarings, multiplies):
     return 2 * L * L * (squarings + multiplies)
 
 
+DEC_WINDOW = 5     # csrc/paillier_sliced.hip kDecWin (efl_pl_tune(ln, 2, 1), the default)
+
+
+def window_products(e: int, w: int = DEC_WINDOW):
+    """(squarings, multiplies) of the sliced decryption's sliding-window exponentiation by e
+    (windows of up to w bits ending in a 1 bit, left to right) including its odd-power table
+    (1 squaring + 2^(w-1) - 1 multiplies), walked exactly as m_func does."""
+    def bit(i):
+        return (e >> i) & 1
+    b = e.bit_length() - 1
+    j = max(b - w + 1, 0)
+    while not bit(j):
+        j += 1
+    b = j - 1
+    sq, mul = 1, (1 << (w - 1)) - 1
+    while b >= 0:
+        if not bit(b):
+            sq += 1
+            b -= 1
+            continue
+        j = max(b - w + 1, 0)
+        while not bit(j):
+            j += 1
+        sq += b - j + 1
+        mul += 1
+        b = j - 1
+    return sq, mul
+
+
 def stage_p(args):
     import random
     import efl
@@ -293,7 +322,10 @@ def stage_p(args):
             raise SystemExit("bench: Paillier round trip is wrong")
         # work per element (exact for decrypt's uniform exponents; expected value for the table)
         pm1, qm1 = p - 1, q - 1
-        dec_macs = sum(_mont_macs(k.ln, e.bit_length() - 1, bin(e).count("1") - 1) for e in (pm1, qm1))
+        dec_window = lib.efl_pl_tune(k.ln, 2, -1) == 1 and pc.kernel_slicing(k.ln, True) > 0
+        dec_ops = [window_products(e) if dec_window else (e.bit_length() - 1, bin(e).count("1") - 1)
+                   for e in (pm1, qm1)]
+        dec_macs = sum(_mont_macs(k.ln, sq, mul) for sq, mul in dec_ops)
         # encryption: one table product per non-zero W-bit window of a' (expected count), + g(m)
         rows = -(-8 * a_bytes // W)
         enc_macs = _mont_macs(k.lc, 0, rows * (1 - 2.0 ** -W) + 1)
@@ -304,11 +336,13 @@ def stage_p(args):
             issued = macs
             if name == "decrypt" and fam:     # sliced decryption exponentiates in radix 2^28
                 L28 = pc.limbs28_total(k.ln, k.ln // fam)
-                issued = sum(_mont_macs(L28, e.bit_length() - 1, bin(e).count("1") - 1) for e in (pm1, qm1))
+                issued = sum(_mont_macs(L28, sq, mul) for sq, mul in dec_ops)
             if name == "encrypt" and k.desc.off_table28 >= 0:   # the radix-2^28 table serves encryption
                 issued = _mont_macs(k.desc.n2_28_len, 0, rows * (1 - 2.0 ** -W) + 1)
             res[name] = {"elements_per_s": round(per_s), "ms": round(times[name] * 1e3, 3),
                          "macs_per_element": int(macs),
+                         "method": ("sliding window w=%d" % DEC_WINDOW if dec_window else "binary")
+                         if name == "decrypt" else "fixed-base table, W=%d" % W,
                          "roofline": {"bound": "valu", "achieved": round(per_s * macs / 1e12, 3),
                                       "peak": round(MAD_U64_U32_PEAK / 1e12, 3), "unit": "TMAC/s",
                                       "frac": round(per_s * macs / MAD_U64_U32_PEAK, 4),

@@ -1109,6 +1109,11 @@ EFL_API int efl_pl_matmul(const void* key_block, const efl_pl_key* key, const ui
 
 EFL_API int efl_pl_tune(int ln, int decrypt, int limbs_per_lane) {
   if (ln != 16 && ln != 32 && ln != 64 && ln != 128) { set_error("unsupported limb count %d", ln); return EFL_E_INVALID_ARGUMENT; }
+  if (decrypt == 2) {   // sliced decryption's exponentiation: 1 sliding window (default), 0 binary
+    if (limbs_per_lane < 0) return pl::sl_dec_window(-1);
+    if (limbs_per_lane > 1) { set_error("decryption method must be 0 (binary) or 1 (window)"); return EFL_E_INVALID_ARGUMENT; }
+    return pl::sl_dec_window(limbs_per_lane);
+  }
   const int dec = decrypt ? 1 : 0;
   if (limbs_per_lane == -2) {                       // back to the measured default, sized per launch
     const int prev = slicing(ln, dec);

@@ -10,6 +10,8 @@
 // Every element owns LDS arrays (limb i of array A at A[i*E]) for its b operands: squaring scratch,
 // the exponentiation base, the fixed-base table entry, running products. All G lanes read the
 // same word (broadcast); the E elements of the wave hit consecutive banks.
+#include <atomic>
+
 #include "pl_common.h"
 #include "sliced.h"
 #include "sliced28.h"
@@ -674,10 +676,32 @@ __global__ __launch_bounds__(kSlBlock) SL_OCC void k_matmul(Key k, const uint32_
 // decryption: L = ln limbs (x^2 for x = p, q), half slices of C/2 limbs for numbers mod x
 // ------------------------------------------------------------------------------------------
 
-// res = L_x(c^(x-1) mod x^2) * h mod x   (paillier.cc:28-48)
+// Sliding-window exponentiation by the decryption exponent x - 1 (the same for every element, so
+// the window walk is wave-uniform): the element's odd powers c^1, c^3, ..., c^(2^kDecWin - 1) in
+// radix-2^28 Montgomery form go to a global scratch slab (kDecEntries x G x CP words per element,
+// this lane's CP-word slice at +g*CP), and every multiply stages its entry in LDS. Products per
+// modulus: bits(x-1) - 1 squarings + ~bits/(kDecWin+1) multiplies + 2^(kDecWin-1) for the table,
+// against bits - 1 + popcount - 1 for the binary method: 2404 instead of ~3071 at 4096-bit n.
+constexpr int kDecWin = 5, kDecEntries = 1 << (kDecWin - 1);
+
+template <int C28>
+__device__ __forceinline__ void store28(uint32_t* __restrict__ q, const uint32_t (&t)[C28]) {
+  constexpr int CP = pad4<C28>();
+#pragma unroll
+  for (int j = 0; j < CP; j += 4)
+    *reinterpret_cast<uint4*>(q + j) = make_uint4(t[j], j + 1 < C28 ? t[j + 1] : 0u, j + 2 < C28 ? t[j + 2] : 0u,
+                                                  j + 3 < C28 ? t[j + 3] : 0u);
+}
+
+// bit b of the uniform exponent
+__device__ __forceinline__ uint32_t ebit(const uint32_t* ex, int b) { return (ex[b >> 5] >> (b & 31)) & 1u; }
+
+// res = L_x(c^(x-1) mod x^2) * h mod x   (paillier.cc:28-48). tab: this element's odd-power slab
+// (sliding window), or null for the binary method.
 template <int C, int G>
 __device__ __forceinline__ void m_func(uint32_t (&res)[C / 2], const uint32_t* __restrict__ c, const Key& k,
-                                       bool second, uint32_t* BASE, uint32_t* SCR, int E, int g) {
+                                       bool second, uint32_t* BASE, uint32_t* SCR, int E, int g,
+                                       uint32_t* __restrict__ tab) {
   constexpr int L = C * G, CH = C / 2, LH = L / 2;
   uint32_t x2[C];
   slice_uniform<C>(x2, k.at(second ? k.d.off_q2 : k.d.off_p2), g);
@@ -713,11 +737,60 @@ __device__ __forceinline__ void m_func(uint32_t (&res)[C / 2], const uint32_t* _
   s28::mont_mul<C28, G>(a, Uniform{k.at(second ? k.d.off_q2_r2_28[kLog2G] : k.d.off_p2_r2_28[kLog2G])}, m28,
                         minv28, g);
   lds_sync();
-  to_lds<C28>(BASE, E, g, a);
+  if (tab) {
+    constexpr int CP = pad4<C28>();
+    uint32_t* slot = tab + g * CP;                 // entry e at slot + e * G * CP
+    // odd powers: T[0] = c, T[e] = T[e-1] c^2
+    store28<C28>(slot, a);
+    uint32_t c2[C28];
+#pragma unroll
+    for (int j = 0; j < C28; ++j) c2[j] = a[j];
+    s28::mont_sqr<C28, G>(c2, SCR, E, m28, minv28, g);
+    lds_sync();
+    to_lds<C28>(BASE, E, g, c2);
+    lds_sync();
 #pragma unroll 1
-  for (int b = ebits - 2; b >= 0; --b) {
-    s28::mont_sqr<C28, G>(a, SCR, E, m28, minv28, g);
-    if ((ex[b >> 5] >> (b & 31)) & 1u) s28::mont_mul<C28, G>(a, LdsElem{BASE, E}, m28, minv28, g);
+    for (int e2 = 1; e2 < kDecEntries; ++e2) {
+      s28::mont_mul<C28, G>(a, LdsElem{BASE, E}, m28, minv28, g);
+      store28<C28>(slot + (size_t)e2 * G * CP, a);
+    }
+    lds_sync();
+    // left to right: windows of up to kDecWin bits that end in a 1 bit (the top bit is 1)
+    int b = ebits - 1;
+    int j = b - kDecWin + 1 > 0 ? b - kDecWin + 1 : 0;
+    while (!ebit(ex, j)) ++j;
+    uint32_t v = 0;
+    for (int t = b; t >= j; --t) v = (v << 1) | ebit(ex, t);
+    load28<C28>(a, slot + (size_t)(v >> 1) * G * CP);
+    b = j - 1;
+#pragma unroll 1
+    while (b >= 0) {
+      if (!ebit(ex, b)) {
+        s28::mont_sqr<C28, G>(a, SCR, E, m28, minv28, g);
+        --b;
+        continue;
+      }
+      j = b - kDecWin + 1 > 0 ? b - kDecWin + 1 : 0;
+      while (!ebit(ex, j)) ++j;
+      v = 0;
+      for (int t = b; t >= j; --t) v = (v << 1) | ebit(ex, t);
+      uint32_t ent[C28];
+      load28<C28>(ent, slot + (size_t)(v >> 1) * G * CP);   // in flight during the squarings
+#pragma unroll 1
+      for (int t = b; t >= j; --t) s28::mont_sqr<C28, G>(a, SCR, E, m28, minv28, g);
+      to_lds<C28>(BASE, E, g, ent);
+      lds_sync();
+      s28::mont_mul<C28, G>(a, LdsElem{BASE, E}, m28, minv28, g);
+      lds_sync();
+      b = j - 1;
+    }
+  } else {
+    to_lds<C28>(BASE, E, g, a);
+#pragma unroll 1
+    for (int b = ebits - 2; b >= 0; --b) {
+      s28::mont_sqr<C28, G>(a, SCR, E, m28, minv28, g);
+      if (ebit(ex, b)) s28::mont_mul<C28, G>(a, LdsElem{BASE, E}, m28, minv28, g);
+    }
   }
   s28::mont_mul<C28, G>(a, Unit{}, m28, minv28, g);   // y = c^(x-1) mod x^2 (< x^2; y = 1 mod x, so y >= 1)
   lds_sync();
@@ -768,7 +841,7 @@ __device__ __forceinline__ void m_func(uint32_t (&res)[C / 2], const uint32_t* _
 template <int C, int G>
 __global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_decrypt(Key k, const uint32_t* __restrict__ ct,
                                                       uint32_t* __restrict__ mag, signed char* __restrict__ neg,
-                                                      long long N) {
+                                                      long long N, uint32_t* __restrict__ win) {
   constexpr int L = C * G, E = kSlBlock / G, CH = C / 2, LH = L / 2;
   constexpr int L28 = s28::limbs_per_lane(L, G) * G;   // LDS arrays also hold radix-2^28 numbers
   extern __shared__ uint32_t lds[];
@@ -777,9 +850,11 @@ __global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_decry
   uint32_t* BASE = lds + e;
   uint32_t* SCR = lds + L28 * E + e;
   const uint32_t* c = ct + i * 2 * L;
+  // this element's odd-power slab (p's, then reused for q's)
+  uint32_t* tab = win ? win + (size_t)i * kDecEntries * G * pad4<s28::limbs_per_lane(L, G)>() : nullptr;
   uint32_t mp[CH], mq[CH];
-  m_func<C, G>(mp, c, k, false, BASE, SCR, E, g);
-  m_func<C, G>(mq, c, k, true, BASE, SCR, E, g);
+  m_func<C, G>(mp, c, k, false, BASE, SCR, E, g, tab);
+  m_func<C, G>(mq, c, k, true, BASE, SCR, E, g, tab);
   // CRT (paillier.cc:296-307): h = ((mp - mq) mod p) * (q^-1 mod p) mod p; m = h q + mq
   uint32_t ph[CH], qh[CH], d[CH];
   slice_uniform<CH>(ph, k.at(k.d.off_p), g);
@@ -936,13 +1011,36 @@ hipError_t run_matmul(const Key& k, const uint32_t* X, const long long* xe, cons
                      s, k, X, xe, ym, ye, zpos, zneg, ze, u, v, w);
   return hipGetLastError();
 }
+// Decryption launches in chunks of at most kDecChunk elements, each with a stream-ordered scratch
+// slab for the sliding window's odd powers (kDecEntries x L28-padded words per element, e.g. 9.5 KB
+// at 4096-bit n: 2.4 GiB at most per chunk), taken and released on `s` like efl_pl_matmul's.
+constexpr long long kDecChunk = 1 << 18;
+std::atomic<int> g_dec_window{1};   // efl_pl_tune(ln, 2, 0/1): binary method / sliding window
+
 template <int C, int G>
 hipError_t run_decrypt(const Key& k, const uint32_t* ct, uint32_t* mag, signed char* neg, long long N,
                        hipStream_t s) {
-  hipLaunchKernelGGL((k_decrypt<C, G>), dim3(grid_of(N, G)), dim3(kSlBlock),
-                     (size_t)(2 * s28::limbs_per_lane(C * G, G) * G) * (kSlBlock / G) * 4, s, k, ct,
-                     mag, neg, N);
-  return hipGetLastError();
+  constexpr int L = C * G;
+  constexpr size_t slab = (size_t)kDecEntries * G * pad4<s28::limbs_per_lane(L, G)>();
+  const size_t lds = (size_t)(2 * s28::limbs_per_lane(L, G) * G) * (kSlBlock / G) * 4;
+  const long long chunk = N < kDecChunk ? N : kDecChunk;
+  uint32_t* win = nullptr;
+  if (g_dec_window.load(std::memory_order_relaxed)) {
+    const hipError_t err = hipMallocAsync(reinterpret_cast<void**>(&win), (size_t)chunk * slab * 4, s);
+    if (err != hipSuccess) return err;
+  }
+  hipError_t err = hipSuccess;
+  for (long long o = 0; o < N && err == hipSuccess; o += chunk) {
+    const long long n = N - o < chunk ? N - o : chunk;
+    hipLaunchKernelGGL((k_decrypt<C, G>), dim3(grid_of(n, G)), dim3(kSlBlock), lds, s, k, ct + o * 2 * L,
+                       mag + o * L, neg + o, n, win);
+    err = hipGetLastError();
+  }
+  if (win) {
+    const hipError_t ferr = hipFreeAsync(win, s);
+    if (err == hipSuccess) err = ferr;
+  }
+  return err;
 }
 
 }  // namespace
@@ -1013,6 +1111,9 @@ hipError_t sl_matmul(const Key& k, int C, const uint32_t* X, const long long* xe
     SL_DISPATCH(2 * k.d.ln, C, (run_matmul28<CC, GG>(k, X, xe, ym, ye, zpos, zneg, ze, u, v, w, s)))
   }
   SL_DISPATCH(2 * k.d.ln, C, (run_matmul<CC, GG>(k, X, xe, ym, ye, zpos, zneg, ze, u, v, w, s)))
+}
+int sl_dec_window(int v) {
+  return v < 0 ? g_dec_window.load() : g_dec_window.exchange(v ? 1 : 0);
 }
 hipError_t sl_decrypt(const Key& k, int C, const uint32_t* ct, uint32_t* mag, signed char* neg, long long N,
                       hipStream_t s) {

@@ -100,6 +100,9 @@ hipError_t sl_matmul(const Key& k, int C, const uint32_t* X, const long long* xe
                      hipStream_t s);
 hipError_t sl_decrypt(const Key& k, int C, const uint32_t* ct, uint32_t* mag, signed char* neg, long long N,
                       hipStream_t s);
+// sliced decryption's exponentiation method: 1 sliding window (default), 0 binary; v < 0 queries.
+// Returns the previous setting.
+int sl_dec_window(int v);
 
 }  // namespace pl
 }  // namespace efl

@@ -11,7 +11,7 @@
  * Conventions
  *  - Every payload pointer is DEVICE memory owned by the caller; the library never synchronises:
  *    work is enqueued on `stream` (NULL = default stream). It allocates nothing except the
- *    stream-ordered scratch of efl_pl_matmul (see there).
+ *    stream-ordered scratch of efl_pl_matmul and of the sliced efl_pl_decrypt (see there).
  *  - Return value: 0 on success, otherwise the NEGATED TensorFlow error code
  *    (tensorflow/core/lib/core/error_codes.proto; the reference reports errors as TF Status):
  *      -3 INVALID_ARGUMENT, -8 RESOURCE_EXHAUSTED, -9 FAILED_PRECONDITION, -10 ABORTED,
@@ -211,7 +211,9 @@ int efl_pl_fbpowm(const void* key_block, const efl_pl_key* key, const uint32_t* 
 /*
  * PaillierDecrypt (paillier.cc:505-561, _Decrypt :296-312): CRT decryption of [n][2*ln]
  * ciphertexts into |m| ([n][ln] limbs) and negative[i] = (m < 0) where m > ceil(2n/3) maps to
- * m - n. ABORTED "No private key." without p, q. n of up to 4096 bits.
+ * m - n. ABORTED "No private key." without p, q. n of up to 4096 bits. The sliced kernels take a
+ * stream-ordered scratch slab for the sliding-window exponentiation (efl_pl_tune decrypt = 2); a
+ * failed allocation returns the HIP error.
  */
 int efl_pl_decrypt(const void* key_block, const efl_pl_key* key, const uint32_t* ciphertext,
                    uint32_t* magnitude, int8_t* negative, int64_t n, void* stream);
@@ -248,7 +250,11 @@ int efl_pl_matmul(const void* key_block, const efl_pl_key* key, const uint32_t* 
  * decryption); -1 queries; -2 restores the default. Returns the previous choice, or a negative
  * error code. Results are identical across families; only speed differs. With the default
  * (never set, or restored by -2) a decryption of too few elements to give every SIMD a wave takes
- * more lanes per element; a family set explicitly is used for every size. */
+ * more lanes per element; a family set explicitly is used for every size. decrypt = 2 selects the
+ * sliced decryption's exponentiation instead: limbs_per_lane 1 = sliding 5-bit windows over odd
+ * powers kept in a stream-ordered scratch slab (default; hipMallocAsync / hipFreeAsync on the
+ * caller's stream, up to 2^18 elements x 16 entries per launch), 0 = binary square-and-multiply
+ * (no scratch), -1 queries. */
 int efl_pl_tune(int ln, int decrypt, int limbs_per_lane);
 
 /* mpz_get_str(..., 16) of n numbers ([n][limbs_per_elem], optional sign bytes): first the text

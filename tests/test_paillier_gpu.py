@@ -80,6 +80,25 @@ def test_decrypt_kat(efl, k, c):
     assert got == [v["m"] for v in vs]
 
 
+@pytest.mark.parametrize("k,c", [p for p in fams(ALL, decrypt=True) if p.values[1]])
+def test_decrypt_kat_binary_method(efl, k, c):
+    """The sliced decryption's two exponentiation methods (efl_pl_tune(ln, 2, .)): sliding 5-bit
+    windows over per-element odd powers (default) and binary square-and-multiply agree with GMP."""
+    lib = efl.lib.raw()
+    ln = k["n_bytes"] // 4
+    kp = keypair(efl, k)
+    vs = k["vectors"]
+    hx = efl.HexTensor.from_strings([v["c"] for v in vs])
+    assert lib.efl_pl_tune(ln, 2, -1) == 1
+    prev = lib.efl_pl_tune(ln, 2, 0)
+    try:
+        with family(ln, True, c):
+            got = kp.decrypt(hx, dtype=torch.int64).cpu().tolist()
+    finally:
+        lib.efl_pl_tune(ln, 2, prev)
+    assert got == [v["m"] for v in vs]
+
+
 @pytest.mark.parametrize("k,c", fams(ALL))
 def test_fbpowm_kat(efl, k, c):
     for g in sorted({v["g"] for v in k["vectors"]}):
