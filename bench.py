@@ -371,6 +371,7 @@ def stage_p(args):
 # x @ fixedpoint_encode(w, decrease_precision=True)): x [256, 28*14] encrypted by the sender
 # (leader_dense.py:44 / follower_dense.py:23 batch 256), w [392, 128] glorot-uniform
 STAGE_P_MATMUL = (256, 392, 128)
+MATMUL_WINDOW = 4   # csrc/paillier_sliced.hip kMatWin
 
 
 def stage_p_matmul(args, efl, pc, kp, lib, sh, stream, dev):
@@ -422,13 +423,23 @@ def stage_p_matmul(args, efl, pc, kp, lib, sh, stream, dev):
         hit = (ay >> q) & 1
         pop += hit
         bits = np.where(hit == 1, q + 1, bits)
+    # multiplies per term: one per right-to-left window of MATMUL_WINDOW bits starting at a 1 bit
+    # (csrc/paillier_sliced.hip k_wmask / kMatWin), not one per set bit
+    nwin = np.zeros(ym_h.shape, dtype=np.int64)
+    rest = ay.copy()
+    while rest.any():
+        low = rest & -rest                                     # lowest set bit
+        has = rest != 0
+        nwin += has
+        rest = np.where(has, rest & ~((low << MATMUL_WINDOW) - 1), 0)
     L = k.lc
     fam = pc.kernel_slicing(k.ln, False)
     # the term split of run_matmul28 (csrc/paillier_sliced.hip): each split squares on its own
     S, G = 1, (L // fam if fam else 1)
     while 2 * S <= 8 and 2 * S <= v and u * w * G * S < 256 * 4 * 64 * 8:
         S *= 2
-    products = u * v + (2 * S * u * w if S > 1 else 0)      # x R; combining the partials + conversion out
+    # x R and its odd powers (1 squaring + 2^(w-1) - 1 products); combining the partials + conversion out
+    products = u * v * (1 + (1 << (MATMUL_WINDOW - 1))) + (2 * S * u * w if S > 1 else 0)
     for sp in range(S):
         j0, j1 = v * sp // S, v * (sp + 1) // S
         for sgn in (1, -1):
@@ -437,7 +448,7 @@ def stage_p_matmul(args, efl, pc, kp, lib, sh, stream, dev):
             top = np.where(mask[None, :, :], d + bits[None, :, :], 0).max(axis=1)    # [u, w]
             started = mask.any(axis=0)[None, :].repeat(u, axis=0)
             # squarings below the top level, multiplies less the first (a copy), one conversion out
-            products += int(np.maximum(top - 1, 0)[started].sum()) + u * int(pop[mask].sum()) - int(started.sum())
+            products += int(np.maximum(top - 1, 0)[started].sum()) + u * int(nwin[mask].sum()) - int(started.sum())
             if S == 1:
                 products += int(started.sum())
     per_term = u * int((bits + pop)[nz].sum()) + int((d * nz[None, :, :]).sum()) + 2 * u * w

@@ -437,22 +437,74 @@ __global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_powm2
 template <int C28>
 constexpr int pad4() { return (C28 + 3) & ~3; }
 
-template <int C, int G>
-__global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_tomont28(Key k, const uint32_t* __restrict__ X,
-                                                                         uint32_t* __restrict__ Xm, long long N) {
-  constexpr int L = C * G, E = kSlBlock / G;
-  constexpr int C28 = s28::limbs_per_lane(L, G), CP = pad4<C28>();
-  extern __shared__ uint32_t lds[];
-  SL_ELEMENT(E, G)
-  if (i >= N) return;
-  uint32_t m28[C28], t[C28];
-  slice_uniform<C28>(m28, k.at(k.d.off_n2_28), g);
-  to_mont28<C, G>(t, X + i * L, k, m28, lds + e, E, g);
-  uint32_t* q = Xm + i * (long long)(CP * G) + g * CP;
+template <int C28>
+__device__ __forceinline__ void store28(uint32_t* __restrict__ q, const uint32_t (&t)[C28]) {
+  constexpr int CP = pad4<C28>();
 #pragma unroll
   for (int j = 0; j < CP; j += 4)
     *reinterpret_cast<uint4*>(q + j) = make_uint4(t[j], j + 1 < C28 ? t[j + 1] : 0u, j + 2 < C28 ? t[j + 2] : 0u,
                                                   j + 3 < C28 ? t[j + 3] : 0u);
+}
+
+// Windowed terms (round 2): every term's exponent |y| is cut right to left into windows of up to
+// kMatWin bits that start at a 1 bit (a window (s, v): bits s .. s + kMatWin - 1 of |y|, v odd), so
+// x^|y| = prod over its windows of (x^v)^(2^s). Each x element gets its odd powers x, x^3, ...,
+// x^(2^kMatWin - 1) once (k_tomont28: 1 squaring + 2^(kMatWin-1) - 1 products, shared by all w
+// outputs of its row), and a term costs one multiply per window instead of one per set bit:
+// ~2.5-3 instead of ~5.5 for the 11-bit mantissas decrease_precision leaves.
+constexpr int kMatWin = 4, kMatEntries = 1 << (kMatWin - 1);
+
+// window starts of |y| (bit s set = a window begins at bit s), right to left
+__global__ __launch_bounds__(256) void k_wmask(const long long* __restrict__ ym, unsigned long long* __restrict__ wm,
+                                               long long n) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const long long y = ym[i];
+  uint64_t ay = y < 0 ? 0ull - (uint64_t)y : (uint64_t)y;
+  uint64_t mask = 0;
+  int s = 0;
+  while (ay >> s) {
+    if ((ay >> s) & 1ull) {
+      mask |= 1ull << s;
+      s += kMatWin;
+    } else {
+      ++s;
+    }
+    if (s >= 64) break;
+  }
+  wm[i] = mask;
+}
+
+// x R mod n^2 and its odd powers (radix 2^28, Montgomery) for every x element:
+// entry e of element i at Xm + (i * kMatEntries + e) * (CP * G), lane g's slice at + g * CP
+template <int C, int G>
+__global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_tomont28(Key k, const uint32_t* __restrict__ X,
+                                                                         uint32_t* __restrict__ Xm, long long N) {
+  constexpr int L = C * G, E = kSlBlock / G;
+  constexpr int C28 = s28::limbs_per_lane(L, G), L28 = C28 * G, CP = pad4<C28>();
+  extern __shared__ uint32_t lds[];
+  SL_ELEMENT(E, G)
+  if (i >= N) return;
+  uint32_t* B = lds + e;
+  uint32_t* SCR = lds + L28 * E + e;
+  uint32_t m28[C28], t[C28], x2[C28];
+  slice_uniform<C28>(m28, k.at(k.d.off_n2_28), g);
+  const uint32_t minv28 = k.d.n2_minv28;
+  to_mont28<C, G>(t, X + i * L, k, m28, B, E, g);
+  uint32_t* q = Xm + i * (long long)kMatEntries * (CP * G) + g * CP;
+  store28<C28>(q, t);
+#pragma unroll
+  for (int j = 0; j < C28; ++j) x2[j] = t[j];
+  lds_sync();
+  s28::mont_sqr<C28, G>(x2, SCR, E, m28, minv28, g);
+  lds_sync();
+  to_lds<C28>(B, E, g, x2);
+  lds_sync();
+#pragma unroll 1
+  for (int e2 = 1; e2 < kMatEntries; ++e2) {
+    s28::mont_mul<C28, G>(t, LdsElem{B, E}, m28, minv28, g);
+    store28<C28>(q + (long long)e2 * (CP * G), t);
+  }
 }
 
 template <int C28>
@@ -472,7 +524,8 @@ template <int C, int G>
 __global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_matmul28(
     Key k, const uint32_t* __restrict__ Xm, const long long* __restrict__ xe, const long long* __restrict__ ym,
     const long long* __restrict__ ye, uint32_t* __restrict__ zpos, uint32_t* __restrict__ zneg,
-    long long* __restrict__ ze, int u, int v, int w, int S, uint32_t* __restrict__ P) {
+    long long* __restrict__ ze, int u, int v, int w, int S, uint32_t* __restrict__ P,
+    const unsigned long long* __restrict__ wmask) {
   constexpr int L = C * G, E = kSlBlock / G;
   constexpr int C28 = s28::limbs_per_lane(L, G), L28 = C28 * G, CP = pad4<C28>();
   extern __shared__ uint32_t lds[];
@@ -489,6 +542,7 @@ __global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_matmu
   const long long* xr = xe + (long long)row * v;
   const long long* yc = ym + kk;
   const long long* ec = ye + kk;
+  const unsigned long long* wc = wmask + kk;
   long long mn = 0x7FFFFFFFFFFFFFFFll;
   for (int j = 0; j < v; ++j) {
     const long long ex = xr[j] + ec[(long long)j * w];
@@ -505,14 +559,15 @@ __global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_matmu
     top = lvl > top ? lvl : top;
   }
   // Each group walks its own event list: per bit level from the top, a squaring of each started
-  // product, then one multiply per term whose exponent has that bit. Every pass of the loop below
-  // is one Montgomery product per group (its first operand from LDS for a squaring, from HBM for a
-  // multiply), so a wave runs max_group(events) products, not the union of its groups' levels.
+  // product, then one multiply per term with a window starting at that level (by the term's odd
+  // power x^v, v the window's value). Every pass of the loop below is one Montgomery product per
+  // group (its first operand from LDS for a squaring, from HBM for a multiply), so a wave runs
+  // max_group(events) products, not the union of its groups' levels.
   bool started0 = false, started1 = false;   // products still 1 take their first term as a copy
   long long b = top - 1;
   int j = 0, phase = 0;                      // phase 0: square POS, 1: square NEG, 2: terms
   for (;;) {
-    int op = -1, jj = 0;                     // op 0/1: square POS/NEG, 2/3: multiply x_j into POS/NEG
+    int op = -1, jj = 0, ent = 0;            // op 0/1: square POS/NEG, 2/3: multiply x_j^v into POS/NEG
     while (op < 0 && b >= 0) {
       if (phase == 0) {
         phase = 1;
@@ -525,14 +580,13 @@ __global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_matmu
         --b;
         phase = 0;
       } else {
-        const long long y = yc[(long long)j * w];
         const long long p = b - (xr[j] + ec[(long long)j * w] - mn);
-        if (y != 0 && p >= 0 && p < 64) {
+        if (p >= 0 && p < 64 && ((wc[(long long)j * w] >> p) & 1ull)) {
+          const long long y = yc[(long long)j * w];
           const uint64_t ay = y < 0 ? 0ull - (uint64_t)y : (uint64_t)y;
-          if ((ay >> p) & 1ull) {
-            op = y < 0 ? 3 : 2;
-            jj = j;
-          }
+          op = y < 0 ? 3 : 2;
+          jj = j;
+          ent = (int)(((ay >> p) & ((1ull << kMatWin) - 1ull)) >> 1);
         }
         ++j;
       }
@@ -540,7 +594,7 @@ __global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_matmu
     if (op < 0) break;
     uint32_t* acc = (op & 1) ? ACC[1] : ACC[0];
     if (op < 2) from_lds<C28>(t, acc, E, g);
-    else load28<C28>(t, Xm + ((long long)row * v + jj) * (CP * G) + g * CP);
+    else load28<C28>(t, Xm + (((long long)row * v + jj) * kMatEntries + ent) * (CP * G) + g * CP);
     const bool copy = op == 2 ? !started0 : op == 3 ? !started1 : false;
     if (!copy) {
       s28::mont_mul<C28, G>(t, LdsElem{acc, E}, m28, minv28, g);
@@ -683,15 +737,6 @@ __global__ __launch_bounds__(kSlBlock) SL_OCC void k_matmul(Key k, const uint32_
 // modulus: bits(x-1) - 1 squarings + ~bits/(kDecWin+1) multiplies + 2^(kDecWin-1) for the table,
 // against bits - 1 + popcount - 1 for the binary method: 2404 instead of ~3071 at 4096-bit n.
 constexpr int kDecWin = 5, kDecEntries = 1 << (kDecWin - 1);
-
-template <int C28>
-__device__ __forceinline__ void store28(uint32_t* __restrict__ q, const uint32_t (&t)[C28]) {
-  constexpr int CP = pad4<C28>();
-#pragma unroll
-  for (int j = 0; j < CP; j += 4)
-    *reinterpret_cast<uint4*>(q + j) = make_uint4(t[j], j + 1 < C28 ? t[j + 1] : 0u, j + 2 < C28 ? t[j + 2] : 0u,
-                                                  j + 3 < C28 ? t[j + 3] : 0u);
-}
 
 // bit b of the uniform exponent
 __device__ __forceinline__ uint32_t ebit(const uint32_t* ex, int b) { return (ex[b >> 5] >> (b & 31)) & 1u; }
@@ -973,15 +1018,25 @@ hipError_t run_matmul28(const Key& k, const uint32_t* X, const long long* xe, co
   int S = 1;
   while (2 * S <= 8 && 2 * S <= v && UW * G * S < kTwoRoundsOfFourWaves) S *= 2;
   const size_t slot = (size_t)pad4<C28>() * G;
-  uint32_t* Xm = nullptr;   // x R mod n^2 in padded radix-2^28 slices, then the partials: stream-ordered scratch
-  hipError_t err = hipMallocAsync(reinterpret_cast<void**>(&Xm), ((size_t)nx + (S > 1 ? (size_t)S * UW * 2 : 0)) * slot * 4, s);
+  // stream-ordered scratch: the odd powers of every x (kMatEntries padded radix-2^28 slices each),
+  // then the S > 1 partials, then the window masks of y
+  const size_t x_words = (size_t)nx * kMatEntries * slot, p_words = S > 1 ? (size_t)S * UW * 2 * slot : 0;
+  const size_t yw = (size_t)v * w;
+  uint32_t* Xm = nullptr;
+  hipError_t err = hipMallocAsync(reinterpret_cast<void**>(&Xm), (x_words + p_words) * 4 + yw * 8, s);
   if (err != hipSuccess) return err;
-  uint32_t* P = S > 1 ? Xm + (size_t)nx * slot : nullptr;
-  hipLaunchKernelGGL((k_tomont28<C, G>), dim3(grid_of(nx, G)), dim3(kSlBlock), (size_t)L28 * E * 4, s, k, X, Xm, nx);
+  uint32_t* P = S > 1 ? Xm + x_words : nullptr;
+  unsigned long long* wm = reinterpret_cast<unsigned long long*>(Xm + x_words + p_words);
+  hipLaunchKernelGGL(k_wmask, dim3((unsigned)((yw + 255) / 256)), dim3(256), 0, s, ym, wm, (long long)yw);
   err = hipGetLastError();
   if (err == hipSuccess) {
+    hipLaunchKernelGGL((k_tomont28<C, G>), dim3(grid_of(nx, G)), dim3(kSlBlock), (size_t)2 * L28 * E * 4, s, k, X, Xm,
+                       nx);
+    err = hipGetLastError();
+  }
+  if (err == hipSuccess) {
     hipLaunchKernelGGL((k_matmul28<C, G>), dim3(grid_of(UW * S, G)), dim3(kSlBlock), (size_t)2 * L28 * E * 4, s, k,
-                       Xm, xe, ym, ye, zpos, zneg, ze, u, v, w, S, P);
+                       Xm, xe, ym, ye, zpos, zneg, ze, u, v, w, S, P, wm);
     err = hipGetLastError();
   }
   if (err == hipSuccess && S > 1) {

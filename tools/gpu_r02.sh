@@ -17,7 +17,8 @@ run() {
     bench2) timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
               --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 3 \
               > gpurun_out/bench2.json 2> gpurun_out/bench2.err ;;
-    pl)     timeout -k 10 600 python -u -m pytest tests/test_paillier_gpu.py tests/test_distributed_gpu.py -m gpu -x -q \
+    pl)     timeout -k 10 600 python -u -m pytest tests/test_paillier_gpu.py tests/test_distributed_gpu.py \
+              tests/test_paillier_layer_gpu.py -m gpu -x -q \
               --timeout 300 --timeout-method thread > gpurun_out/pytest_pl.log 2>&1 ;;
     stagep) timeout -k 10 900 python -u bench.py --stage p --no-cpu-baseline > gpurun_out/stage_p.jsonl 2> gpurun_out/stage_p.err ;;
     hex)    timeout -k 10 240 python -u tools/bench_hex.py > gpurun_out/bench_hex.json 2> gpurun_out/bench_hex.err ;;
