@@ -371,7 +371,7 @@ def stage_p(args):
 # x @ fixedpoint_encode(w, decrease_precision=True)): x [256, 28*14] encrypted by the sender
 # (leader_dense.py:44 / follower_dense.py:23 batch 256), w [392, 128] glorot-uniform
 STAGE_P_MATMUL = (256, 392, 128)
-MATMUL_WINDOW = 4   # csrc/paillier_sliced.hip kMatWin
+MATMUL_WINDOW = 5   # csrc/paillier_sliced.hip kMatWin
 
 
 def stage_p_matmul(args, efl, pc, kp, lib, sh, stream, dev):

@@ -451,8 +451,11 @@ __device__ __forceinline__ void store28(uint32_t* __restrict__ q, const uint32_t
 // x^|y| = prod over its windows of (x^v)^(2^s). Each x element gets its odd powers x, x^3, ...,
 // x^(2^kMatWin - 1) once (k_tomont28: 1 squaring + 2^(kMatWin-1) - 1 products, shared by all w
 // outputs of its row), and a term costs one multiply per window instead of one per set bit:
-// ~2.5-3 instead of ~5.5 for the 11-bit mantissas decrease_precision leaves.
-constexpr int kMatWin = 4, kMatEntries = 1 << (kMatWin - 1);
+// ~2-2.5 instead of ~5.5 for the 11-bit mantissas decrease_precision leaves.
+#ifndef EFL_MAT_WIN
+#define EFL_MAT_WIN 5   // 3 / 4 / 5 / 6: 31.4 / 29.7 / 27.2 / 27.5 ms (profiles/r02/matmul_window_sweep.json)
+#endif
+constexpr int kMatWin = EFL_MAT_WIN, kMatEntries = 1 << (kMatWin - 1);
 
 // window starts of |y| (bit s set = a window begins at bit s), right to left
 __global__ __launch_bounds__(256) void k_wmask(const long long* __restrict__ ym, unsigned long long* __restrict__ wm,
