@@ -57,3 +57,26 @@ def test_two_rank_gloo():
     res = [q.get(timeout=60) for _ in range(2)]
     assert all(r[0] == b"\x07" * 32 and r[1] == {"n": "abc", "hs": "12"} for r in res)
     assert any(r[2] is True for r in res)
+
+
+def test_choose_backend(monkeypatch):
+    """RCCL when every rank has its own GPU (the driver's 8-GPU node), gloo when ranks would share
+    one (RCCL refuses two ranks on a device) or there is none; an explicit choice wins."""
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    assert edist.choose_backend(8) == "nccl" and edist.choose_backend(2) == "nccl"
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    assert edist.choose_backend(2) == "gloo" and edist.choose_backend(1) == "nccl"
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 0)
+    assert edist.choose_backend(1) == "gloo"
+    assert edist.choose_backend(4, "nccl") == "nccl"
+
+
+def test_shard_range_paillier_counters():
+    """shard_keypair starts each rank's Philox counter at its shard's global offset (8-byte
+    elements: 32-element quanta), so the ranks' counter ranges tile [0, n) exactly."""
+    for n in (1, 31, 32, 300, 1000003):
+        for world in (1, 2, 3, 8):
+            rs = [edist.shard_range(n, world, r, elem_bytes=8) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            assert all(e0 == s1 for (_, e0), (s1, _) in zip(rs, rs[1:]))
+            assert all(s % 32 == 0 for s, _ in rs if s < n)
