@@ -436,8 +436,14 @@ def stage_p_matmul(args, efl, pc, kp, lib, sh, stream, dev):
     fam = pc.kernel_slicing(k.ln, False)
     # the term split of run_matmul28 (csrc/paillier_sliced.hip): each split squares on its own
     S, G = 1, (L // fam if fam else 1)
-    while 2 * S <= 8 and 2 * S <= v and u * w * G * S < 256 * 4 * 64 * 8:
-        S *= 2
+    fixed = lib.efl_pl_tune(k.ln, 3, -1)       # efl_pl_tune(ln, 3, S): a fixed split, 0 = per launch
+    if fixed > 0:
+        while 2 * S <= fixed and 2 * S <= v:
+            S *= 2
+    else:
+        waves = 2 if fam >= 32 else 4                    # k_matmul28's waves per SIMD
+        while 2 * S <= 8 and 2 * S <= v and u * w * G * S < 256 * 4 * 64 * 2 * waves:
+            S *= 2
     # x R and its odd powers (1 squaring + 2^(w-1) - 1 products); combining the partials + conversion out
     products = u * v * (1 + (1 << (MATMUL_WINDOW - 1))) + (2 * S * u * w if S > 1 else 0)
     for sp in range(S):

@@ -143,6 +143,19 @@ __device__ __forceinline__ void fbpowm_mont(uint32_t (&acc)[C], const Key& k, ui
 #define EFL_DEC_WAVES 4
 #endif
 
+// k_matmul28's waves per SIMD (build knobs EFL_MAT_WAVES16 / EFL_MAT_WAVES32) and whether its event
+// loop loads the next multiply's operand while the current product runs (EFL_MAT_PREFETCH: C28
+// more registers, so it pays only where the register cap leaves room)
+#ifndef EFL_MAT_WAVES16
+#define EFL_MAT_WAVES16 EFL_DEC_WAVES
+#endif
+#ifndef EFL_MAT_WAVES32
+#define EFL_MAT_WAVES32 2
+#endif
+#ifndef EFL_MAT_PREFETCH
+#define EFL_MAT_PREFETCH 0
+#endif
+
 #define SL_ELEMENT(E_, G_)                                   \
   const int g = (int)threadIdx.x % (G_);                     \
   const int e = (int)threadIdx.x / (G_);                     \
@@ -456,6 +469,9 @@ __device__ __forceinline__ void store28(uint32_t* __restrict__ q, const uint32_t
 #define EFL_MAT_WIN 5   // 3 / 4 / 5 / 6: 31.4 / 29.7 / 27.2 / 27.5 ms (profiles/r02/matmul_window_sweep.json)
 #endif
 constexpr int kMatWin = EFL_MAT_WIN, kMatEntries = 1 << (kMatWin - 1);
+// term splits of efl_pl_matmul: 0 = chosen per launch (run_matmul28), else a fixed power of two
+// (efl_pl_tune(ln, 3, S))
+std::atomic<int> g_mat_splits{0};
 
 // window starts of |y| (bit s set = a window begins at bit s), right to left
 __global__ __launch_bounds__(256) void k_wmask(const long long* __restrict__ ym, unsigned long long* __restrict__ wm,
@@ -524,7 +540,7 @@ __device__ __forceinline__ void load28(uint32_t (&t)[C28], const uint32_t* __res
 }
 
 template <int C, int G>
-__global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_matmul28(
+__global__ __launch_bounds__(kSlBlock, C >= 32 ? EFL_MAT_WAVES32 : EFL_MAT_WAVES16) void k_matmul28(
     Key k, const uint32_t* __restrict__ Xm, const long long* __restrict__ xe, const long long* __restrict__ ym,
     const long long* __restrict__ ye, uint32_t* __restrict__ zpos, uint32_t* __restrict__ zneg,
     long long* __restrict__ ze, int u, int v, int w, int S, uint32_t* __restrict__ P,
@@ -569,8 +585,12 @@ __global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_matmu
   bool started0 = false, started1 = false;   // products still 1 take their first term as a copy
   long long b = top - 1;
   int j = 0, phase = 0;                      // phase 0: square POS, 1: square NEG, 2: terms
-  for (;;) {
-    int op = -1, jj = 0, ent = 0;            // op 0/1: square POS/NEG, 2/3: multiply x_j^v into POS/NEG
+  // The next event of this group's list: op 0/1 square POS/NEG, 2/3 multiply x_j^v into POS/NEG,
+  // -1 at the end; `addr` = the multiply's operand in Xm, `copy` = it is its product's first term
+  // (a product counts as started once its first multiply has been scanned).
+  auto next = [&](int& op, long long& addr, bool& copy) {
+    op = -1;
+    copy = false;
     while (op < 0 && b >= 0) {
       if (phase == 0) {
         phase = 1;
@@ -587,27 +607,68 @@ __global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_matmu
         if (p >= 0 && p < 64 && ((wc[(long long)j * w] >> p) & 1ull)) {
           const long long y = yc[(long long)j * w];
           const uint64_t ay = y < 0 ? 0ull - (uint64_t)y : (uint64_t)y;
-          op = y < 0 ? 3 : 2;
-          jj = j;
-          ent = (int)(((ay >> p) & ((1ull << kMatWin) - 1ull)) >> 1);
+          const int ent = (int)(((ay >> p) & ((1ull << kMatWin) - 1ull)) >> 1);
+          addr = (((long long)row * v + j) * kMatEntries + ent) * (CP * G) + g * CP;
+          if (y < 0) {
+            op = 3;
+            copy = !started1;
+            started1 = true;
+          } else {
+            op = 2;
+            copy = !started0;
+            started0 = true;
+          }
         }
         ++j;
       }
     }
-    if (op < 0) break;
+  };
+  int op;
+  long long addr = 0;
+  bool copy;
+#if EFL_MAT_PREFETCH
+  // scanned one event ahead: the next multiply's HBM operand loads while this product computes
+  int op_n;
+  long long addr_n = 0;
+  bool copy_n;
+  uint32_t nx[C28];
+  next(op, addr, copy);
+  if (op >= 2) load28<C28>(nx, Xm + addr);
+  while (op >= 0) {
     uint32_t* acc = (op & 1) ? ACC[1] : ACC[0];
-    if (op < 2) from_lds<C28>(t, acc, E, g);
-    else load28<C28>(t, Xm + (((long long)row * v + jj) * kMatEntries + ent) * (CP * G) + g * CP);
-    const bool copy = op == 2 ? !started0 : op == 3 ? !started1 : false;
+    if (op < 2) {
+      from_lds<C28>(t, acc, E, g);
+    } else {
+#pragma unroll
+      for (int q = 0; q < C28; ++q) t[q] = nx[q];
+    }
+    next(op_n, addr_n, copy_n);
+    if (op_n >= 2) load28<C28>(nx, Xm + addr_n);
     if (!copy) {
       s28::mont_mul<C28, G>(t, LdsElem{acc, E}, m28, minv28, g);
       lds_sync();
     }
     to_lds<C28>(acc, E, g, t);
     lds_sync();
-    if (op == 2) started0 = true;
-    if (op == 3) started1 = true;
+    op = op_n;
+    addr = addr_n;
+    copy = copy_n;
   }
+#else
+  for (;;) {
+    next(op, addr, copy);
+    if (op < 0) break;
+    uint32_t* acc = (op & 1) ? ACC[1] : ACC[0];
+    if (op < 2) from_lds<C28>(t, acc, E, g);
+    else load28<C28>(t, Xm + addr);
+    if (!copy) {
+      s28::mont_mul<C28, G>(t, LdsElem{acc, E}, m28, minv28, g);
+      lds_sync();
+    }
+    to_lds<C28>(acc, E, g, t);
+    lds_sync();
+  }
+#endif
   if (S > 1) {
     // partial products (radix-2^28 Montgomery form, < 2m) for k_matcomb28; 1 = R for an unused sign
 #pragma unroll
@@ -1015,11 +1076,18 @@ hipError_t run_matmul28(const Key& k, const uint32_t* X, const long long* xe, co
   constexpr int C28 = s28::limbs_per_lane(C * G, G), L28 = C28 * G, E = kSlBlock / G;
   const long long nx = (long long)u * v, UW = (long long)u * w;
   // terms split S ways over separate groups when one group per output would give fewer than two
-  // rounds of 4 waves per SIMD (the occupancy the register bound allows; a second round evens out
-  // the groups' unequal event counts); partials combined after. bench.py mirrors this choice.
-  constexpr long long kTwoRoundsOfFourWaves = 256ll * 4 * 64 * 8;
+  // rounds of the kernel's waves per SIMD (a second round evens out the groups' unequal event
+  // counts; more splits repeat each split's squarings: 1034 / 1133 / 1324 products per output of
+  // the MNIST product at S = 2 / 4 / 8, profiles/r02/matmul_splits.jsonl); partials combined after.
+  // bench.py mirrors this choice.
+  constexpr long long kTwoRounds = 256ll * 4 * 64 * 2 * (C >= 32 ? EFL_MAT_WAVES32 : EFL_MAT_WAVES16);
   int S = 1;
-  while (2 * S <= 8 && 2 * S <= v && UW * G * S < kTwoRoundsOfFourWaves) S *= 2;
+  const int fixed = g_mat_splits.load();
+  if (fixed > 0) {
+    while (2 * S <= fixed && 2 * S <= v) S *= 2;
+  } else {
+    while (2 * S <= 8 && 2 * S <= v && UW * G * S < kTwoRounds) S *= 2;
+  }
   const size_t slot = (size_t)pad4<C28>() * G;
   // stream-ordered scratch: the odd powers of every x (kMatEntries padded radix-2^28 slices each),
   // then the S > 1 partials, then the window masks of y
@@ -1172,6 +1240,9 @@ hipError_t sl_matmul(const Key& k, int C, const uint32_t* X, const long long* xe
 }
 int sl_dec_window(int v) {
   return v < 0 ? g_dec_window.load() : g_dec_window.exchange(v ? 1 : 0);
+}
+int sl_mat_splits(int v) {
+  return v < 0 ? g_mat_splits.load() : g_mat_splits.exchange(v);
 }
 hipError_t sl_decrypt(const Key& k, int C, const uint32_t* ct, uint32_t* mag, signed char* neg, long long N,
                       hipStream_t s) {

@@ -103,6 +103,9 @@ hipError_t sl_decrypt(const Key& k, int C, const uint32_t* ct, uint32_t* mag, si
 // sliced decryption's exponentiation method: 1 sliding window (default), 0 binary; v < 0 queries.
 // Returns the previous setting.
 int sl_dec_window(int v);
+// efl_pl_matmul's term splits: 0 chosen per launch (default), else 1..16 (rounded down to a power of
+// two); v < 0 queries. Returns the previous setting.
+int sl_mat_splits(int v);
 
 }  // namespace pl
 }  // namespace efl

@@ -254,7 +254,9 @@ int efl_pl_matmul(const void* key_block, const efl_pl_key* key, const uint32_t* 
  * sliced decryption's exponentiation instead: limbs_per_lane 1 = sliding 5-bit windows over odd
  * powers kept in a stream-ordered scratch slab (default; hipMallocAsync / hipFreeAsync on the
  * caller's stream, up to 2^18 elements x 16 entries per launch), 0 = binary square-and-multiply
- * (no scratch), -1 queries. */
+ * (no scratch), -1 queries. decrypt = 3 sets efl_pl_matmul's term splits (radix-2^28 family):
+ * limbs_per_lane 0 = chosen per launch (default), 1..16 = that many (rounded down to a power of two,
+ * at most v), -1 queries. */
 int efl_pl_tune(int ln, int decrypt, int limbs_per_lane);
 
 /* mpz_get_str(..., 16) of n numbers ([n][limbs_per_elem], optional sign bytes): first the text

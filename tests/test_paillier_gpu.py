@@ -392,12 +392,38 @@ def _matmul_vs_oracle(efl):
     assert dec == want
 
 
+@pytest.mark.parametrize("splits", [1, 2, 3, 4, 16])
+def test_matmul_term_splits(efl, splits):
+    """efl_pl_tune(ln, 3, S) fixes k_matmul28's term splits (rounded down to a power of two, at
+    most v; S = 1 writes the outputs directly, S > 1 goes through k_matcomb28): the same ciphertexts
+    as the oracle for each."""
+    lib = efl.lib.raw()
+    ln = ENC_KEYS[0]["n_bytes"] // 4
+    prev = lib.efl_pl_tune(ln, 3, splits)
+    try:
+        assert lib.efl_pl_tune(ln, 3, -1) == splits
+        _matmul_vs_oracle(efl)
+    finally:
+        lib.efl_pl_tune(ln, 3, prev)
+    assert lib.efl_pl_tune(ln, 3, 17) < 0
+    assert lib.efl_pl_tune(ln, 3, -1) == prev
+
+
 def test_matmul_many_outputs_plaintext(efl):
-    """Enough outputs that every one gets its own group (no term split, k_matmul28 with S = 1; the
-    small oracle cases above take the split + combine path): exact plaintexts of sampled outputs,
-    both signs, zeros and exponent spreads."""
+    """Many outputs, each output's terms in one group (S = 1, set through efl_pl_tune; the small
+    oracle cases above take the split + combine path by default): exact plaintexts of sampled
+    outputs, both signs, zeros and exponent spreads."""
     k = ENC_KEYS[0]
     kp = keypair(efl, k)
+    lib = efl.lib.raw()
+    prev = lib.efl_pl_tune(k["n_bytes"] // 4, 3, 1)
+    try:
+        _many_outputs(kp)
+    finally:
+        lib.efl_pl_tune(k["n_bytes"] // 4, 3, prev)
+
+
+def _many_outputs(kp):
     rng = np.random.default_rng(11)
     u, v, w = 512, 3, 256
     xm = rng.integers(-2**30, 2**30, (u, v))

@@ -38,6 +38,12 @@ run() {
     e2ebench) timeout -k 10 600 python -u tools/bench_e2e.py > gpurun_out/bench_e2e.json 2> gpurun_out/bench_e2e.err ;;
     bprobe) timeout -k 10 300 python -u tools/batched_probe.py > gpurun_out/batched_probe.json 2> gpurun_out/batched_probe.err ;;
     stagepc) timeout -k 10 1100 python -u bench.py --stage p > gpurun_out/stage_p_cpu.jsonl 2> gpurun_out/stage_p_cpu.err ;;
+    mmsweep) timeout -k 10 600 python -u tools/matmul_sweep.py > gpurun_out/matmul_sweep.jsonl 2> gpurun_out/matmul_sweep.err ;;
+    mmvar)  for v in "" _mmC; do
+              EFL_HIP_LIB=$PWD/elastic-federated-learning-solution_amd/efl/libefl_hip$v.so timeout -k 10 300 \
+                python -u tools/matmul_sweep.py --families 16,32 0 1 2 4 8 >> gpurun_out/matmul_var.jsonl \
+                2>> gpurun_out/matmul_var.err || return 1
+            done ;;
     plfam)  timeout -k 10 600 python -u tools/sweep_pl_family.py > gpurun_out/sweep_pl_family.jsonl 2> gpurun_out/sweep_pl_family.err ;;
     profp)  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_p -o run --output-format csv \
               -- python3 bench.py --stage p --no-cpu-baseline > gpurun_out/prof_p.log 2>&1 ;;
