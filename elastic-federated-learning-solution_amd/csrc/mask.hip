@@ -1,5 +1,6 @@
-// Secret-sharing masks: the additive float noise EFLS applies to a tensor
-// before the communicator sends one share of it cross-silo.
+// Secret-sharing masks and DP-SGD noise: the additive float noise EFLS
+// applies to a tensor before the communicator sends one share of it cross-silo, and the Gaussian
+// noise its DP optimisers add to the summed microbatch gradients.
 //
 // Reference: efls-train/python/efl/privacy/secret_sharing.py
 //   generate_suitable_noise(t) = tf.random.uniform(shape(t)) * t                        (:26-27)
@@ -204,6 +205,59 @@ __global__ __launch_bounds__(kBlock) void k_mask_rows(const float* __restrict__ 
   }
 }
 
+// ---- DP-SGD noise (efls-train/python/efl/privacy/dp_optimizer.py) ------------
+// TF's tf.random.normal (NormalDistribution<PhiloxRandom, float>, tensorflow/core/lib/random/
+// random_distributions.h): every Philox4x32-10 block gives 4 normals, Box-Muller on the word pairs
+// (0, 1) and (2, 3): u1 = max(Uint32ToFloat(x0), 1e-7), v1 = float(2 pi (double) * Uint32ToFloat(x1)),
+// r = sqrt(-2 log u1), (f0, f1) = r (sin v1, cos v1). Element i takes normal i % 4 of block
+// ctr0 + i / 4, as the uniform masks do.
+__device__ __forceinline__ void box_muller(uint32_t x0, uint32_t x1, float& f0, float& f1) {
+  float u1 = u01(x0);
+  if (u1 < 1.0e-7f) u1 = 1.0e-7f;
+  const float v1 = (float)(2.0 * 3.14159265358979323846 * (double)u01(x1));
+  const float r = sqrtf(-2.0f * logf(u1));
+  float sn, cs;
+  sincosf(v1, &sn, &cs);
+  f0 = sn * r;
+  f1 = cs * r;
+}
+
+__device__ __forceinline__ void normal4(uint64_t seed, uint64_t blk, float (&z)[4]) {
+  uint32_t c[4] = {(uint32_t)blk, (uint32_t)(blk >> 32), 0u, 0u};
+  philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  box_muller(c[0], c[1], z[0], z[1]);
+  box_muller(c[2], c[3], z[2], z[3]);
+}
+
+// MODE 0, ElementWiseGaussianSumQuery.add_noise (dp_optimizer.py:70-71): v + normal * v * sigma;
+// MODE 1, GaussianSumQuery (tensorflow_privacy 0.3.0, TF 1.x branch): v + (normal * stddev + 0);
+// then safe_normalize (dp_optimizer.py:210-214): / num_microbatches. Each op rounds on its own.
+template <int MODE>
+__device__ __forceinline__ float dp_one(float v, float z, float sigma, float div) {
+  const float n = MODE == 0 ? (z * v) * sigma : z * sigma + 0.0f;
+  return (v + n) / div;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_dp_noise(const float* x, float* o,   // in place allowed
+                                                     long long n, uint64_t seed, uint64_t ctr0, float sigma,
+                                                     float div) {
+  const long long g = (long long)blockIdx.x * kBlock + threadIdx.x;
+  const long long i0 = g * 4;
+  if (i0 >= n) return;
+  float z[4];
+  normal4(seed, ctr0 + (uint64_t)g, z);
+  if (i0 + 4 <= n) {
+    const f4 v = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + g);
+    f4 r;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[j] = dp_one<MODE>(v[j], z[j], sigma, div);
+    stv(reinterpret_cast<f4*>(o) + g, r);
+  } else {
+    for (int j = 0; j < 4 && i0 + j < n; ++j) o[i0 + j] = dp_one<MODE>(x[i0 + j], z[j], sigma, div);
+  }
+}
+
 unsigned grid_for(long long lanes) { return (unsigned)((lanes + kBlock - 1) / kBlock); }
 
 bool lanes_ok(long long lanes) { return lanes / kBlock < (1ll << 31); }
@@ -268,4 +322,20 @@ EFL_API int efl_ss_mask_rows(const float* b, float* send, float* keep0, float* k
   if (v4) k_mask_rows<4><<<grid_for(lanes), kBlock, 0, s>>>(b, send, keep0, keep1, rows, cols, seed, ctr0);
   else k_mask_rows<1><<<grid_for(lanes), kBlock, 0, s>>>(b, send, keep0, keep1, rows, cols, seed, ctr0);
   return hip_status(hipGetLastError(), "efl_ss_mask_rows");
+}
+
+EFL_API int efl_dp_noise(const float* x, float* out, int64_t n, int mode, float sigma, float divisor, uint64_t seed,
+                         uint64_t ctr0, void* stream) {
+  if (n < 0) { set_error("negative element count"); return EFL_E_INVALID_ARGUMENT; }
+  if (mode < 0 || mode > 1) { set_error("efl_dp_noise: mode must be 0 (element-wise) or 1 (Gaussian sum)"); return EFL_E_INVALID_ARGUMENT; }
+  if (!(divisor == divisor) || divisor == 0.0f) { set_error("efl_dp_noise: divisor must be non-zero"); return EFL_E_INVALID_ARGUMENT; }
+  if (n == 0) return EFL_OK;
+  if (!x || !out) { set_error("null buffer"); return EFL_E_INVALID_ARGUMENT; }
+  if (!aligned(x, 16) || !aligned(out, 16)) { set_error("efl_dp_noise: buffers must be 16-byte aligned"); return EFL_E_INVALID_ARGUMENT; }
+  const long long lanes = (n + 3) / 4;
+  if (!lanes_ok(lanes)) { set_error("efl_dp_noise: tensor too large"); return EFL_E_INVALID_ARGUMENT; }
+  hipStream_t s = (hipStream_t)stream;
+  if (mode == 0) k_dp_noise<0><<<grid_for(lanes), kBlock, 0, s>>>(x, out, n, seed, ctr0, sigma, divisor);
+  else k_dp_noise<1><<<grid_for(lanes), kBlock, 0, s>>>(x, out, n, seed, ctr0, sigma, divisor);
+  return hip_status(hipGetLastError(), "efl_dp_noise");
 }

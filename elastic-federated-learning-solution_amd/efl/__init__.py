@@ -4,6 +4,7 @@ Public names mirror efls-train/python/efl (exporter registry, efl/__init__.py:47
   efl.paillier.fixedpoint.{encode, decode, Tensor}, efl.paillier.{Keypair, Tensor}
   efl.Communicator (gRPC TrainerService, pre-send/post-recv hooks), efl.privacy.FixedPointHook
   efl.secret_sharing.{matmul, Dense, dense, share, reveal}
+  efl.privacy.{DPGradientDescentGaussianOptimizer, DPAdamOptimizer, ..., make_optimizer_class}
   efl.HexTensor (the DT_STRING stand-in), efl.lib.ops (the `fed_ops` namespace)
 The kernels live in libefl_hip.so (C ABI: include/efl_hip.h); there is no CPU fallback.
 """
@@ -11,6 +12,7 @@ from efl import exporter
 from efl import errors
 from efl import lib
 from efl.lib import set_flush_denormal, flush_denormal
+from efl.privacy import dp_optimizer
 from efl.privacy import encryptor_utils
 from efl.privacy import paillier
 from efl.privacy import paillier_cipher

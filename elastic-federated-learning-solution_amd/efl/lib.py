@@ -44,6 +44,8 @@ _SIGS = {
     "efl_ss_noise": ([_vp, _vp, _vp, _i64, _i32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_float, _vp], _i32),
     "efl_ss_mask_cols": ([_vp, _vp, _vp, _vp, _i64, _i64, ctypes.c_uint64, ctypes.c_uint64, _vp], _i32),
     "efl_ss_mask_rows": ([_vp, _vp, _vp, _vp, _i64, _i64, ctypes.c_uint64, ctypes.c_uint64, _vp], _i32),
+    "efl_dp_noise": ([_vp, _vp, _i64, _i32, ctypes.c_float, ctypes.c_float, ctypes.c_uint64, ctypes.c_uint64, _vp],
+                     _i32),
 }
 for _name, (_args, _ret) in _SIGS.items():
     _f = getattr(_lib, _name)

@@ -295,6 +295,17 @@ int efl_ss_mask_cols(const float* a, float* send, float* keep0, float* keep1, in
 int efl_ss_mask_rows(const float* b, float* send, float* keep0, float* keep1, int64_t rows,
                      int64_t cols, uint64_t seed, uint64_t ctr0, void* stream);
 
+/* ---- DP-SGD noise ---------------------------------------------------------
+ * The noise step of efls-train/python/efl/privacy/dp_optimizer.py's DP optimisers over a summed
+ * gradient x (n floats), then safe_normalize's division (:210-214), in one pass:
+ * mode 0 (ElementWiseGaussianSumQuery, :70-71, no l2_norm_clip): out = (x + z * x * sigma) / divisor;
+ * mode 1 (GaussianSumQuery, l2_norm_clip set; sigma = its stddev = clip * noise_multiplier):
+ * out = (x + (z * sigma + 0)) / divisor. z = tf.random.normal's construction (Philox4x32-10, Box-Muller
+ * on word pairs); element i takes normal i % 4 of block ctr0 + i / 4 under `seed`. 16-byte aligned
+ * device buffers; out may equal x. */
+int efl_dp_noise(const float* x, float* out, int64_t n, int mode, float sigma, float divisor, uint64_t seed,
+                 uint64_t ctr0, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -12,6 +12,14 @@ random_distributions.h: exponent 127 over the low 23 bits, minus 1.0). TF's own 
 the reference pins only the distribution; the build fixes the counter layout (element i = word i % 4
 of block ctr0 + i / 4, key = seed) and this oracle follows it, so kernel outputs compare bit for bit.
 The fp32 arithmetic is done in numpy float32 (IEEE round-to-nearest, same as the kernels).
+
+DP-SGD noise (efls-train/python/efl/privacy/dp_optimizer.py:60-73; tensorflow_privacy 0.3.0
+GaussianSumQuery): tf.random.normal is TF's NormalDistribution over the same Philox words --
+Box-Muller on word pairs (0, 1), (2, 3) of each block (BoxMullerFloat: u1 = max(U(x0), 1e-7),
+v1 = float(2 pi * U(x1)) in double, r = sqrt(-2 log u1), (r sin v1, r cos v1)). log/sin/cos here are
+float64 rounded to float32 (correctly rounded); the kernels use the device's logf / sincosf, so the
+normals agree to a few ulp, not bit for bit (the tests state the tolerance). Parity with the
+reference is statistical only: its stream is unseeded.
 """
 import numpy as np
 
@@ -80,3 +88,36 @@ def mask_rows(b: np.ndarray, seed: int, ctr0: int):
     half = (b / np.float32(2)).astype(np.float32)
     send = np.concatenate([half - f, f_even - f_odd], axis=0).astype(np.float32)
     return send, (half + f).astype(np.float32), (f_odd + f_even).astype(np.float32)
+
+
+def normal(seed: int, ctr0: int, n: int) -> np.ndarray:
+    """N(0, 1) float32 for elements 0..n-1 of one call (TF's Box-Muller over Philox word pairs)."""
+    nb = (n + 3) // 4
+    w = philox_blocks(seed, ctr0, nb)
+    u = (np.uint32(0x3F800000) | (w & np.uint32(0x7FFFFF))).view(np.float32) - np.float32(1.0)
+    u = u.astype(np.float32)
+    out = np.empty((nb, 4), np.float32)
+    for a, b in ((0, 1), (2, 3)):
+        u1 = np.maximum(u[:, a], np.float32(1.0e-7)).astype(np.float32)
+        v1 = (2.0 * np.pi * u[:, b].astype(np.float64)).astype(np.float32)
+        lg = np.log(u1.astype(np.float64)).astype(np.float32)
+        r = np.sqrt((np.float32(-2.0) * lg).astype(np.float32).astype(np.float64)).astype(np.float32)
+        sn = np.sin(v1.astype(np.float64)).astype(np.float32)
+        cs = np.cos(v1.astype(np.float64)).astype(np.float32)
+        out[:, a] = sn * r
+        out[:, b] = cs * r
+    return out.reshape(-1)[:n]
+
+
+def dp_noise(x: np.ndarray, seed: int, ctr0: int, mode: int, sigma: float, divisor: float, z=None):
+    """efl_dp_noise: mode 0 (x + z x sigma) / d; mode 1 (x + (z sigma + 0)) / d (float32 steps).
+    `z` overrides the normals (to isolate the arithmetic from log/sin/cos rounding)."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    z = normal(seed, ctr0, x.size).reshape(x.shape) if z is None else np.asarray(z, np.float32).reshape(x.shape)
+    s = np.float32(sigma)
+    with np.errstate(all="ignore"):          # inf * 0 and overflow behave as the fp32 ops do
+        if mode == 0:
+            nz = ((z * x).astype(np.float32) * s).astype(np.float32)
+        else:
+            nz = ((z * s).astype(np.float32) + np.float32(0.0)).astype(np.float32)
+        return ((x + nz).astype(np.float32) / np.float32(divisor)).astype(np.float32)

@@ -9,6 +9,7 @@ Algorithmic bytes per fp32 element (read x once, write every output once):
   share (op 1), weight (op 2)  4 + 4 + 4   = 12 B
   mask_cols (mode A)      4 + 6 + 4 + 2    = 16 B  (send 3/2, keep a - e, keep 1/2)
   mask_rows (mode B)      4 + 6 + 4 + 2    = 16 B
+  dp_noise (efl_dp_noise, both modes: Box-Muller normal, noise, / microbatches)  4 + 4 = 8 B
 """
 import argparse
 import json
@@ -52,6 +53,8 @@ cases = {
     "weight_noise": (12, lambda: lib.efl_ss_noise(xp, p0, p1, n, 2, 7, 0, 2.0, sh)),
     "mask_cols": (16, lambda: lib.efl_ss_mask_cols(xp, send_c.data_ptr(), p0, k1_c.data_ptr(), R, C, 7, 0, sh)),
     "mask_rows": (16, lambda: lib.efl_ss_mask_rows(xp, send_r.data_ptr(), p0, k1_r.data_ptr(), R, C, 7, 0, sh)),
+    "dp_noise_elementwise": (8, lambda: lib.efl_dp_noise(xp, p0, n, 0, 1.0, 256.0, 7, 0, sh)),
+    "dp_noise_gaussian": (8, lambda: lib.efl_dp_noise(xp, p0, n, 1, 1.1, 256.0, 7, 0, sh)),
 }
 
 
@@ -61,7 +64,9 @@ def cpu_sample(name, rows=1024):
     xs = x[:rows].cpu().numpy()
     fn = {"noise": lambda: mask.noise(xs, 7, 0, 0), "share": lambda: mask.noise(xs, 7, 0, 1),
           "weight_noise": lambda: mask.noise(xs, 7, 0, 2, 2.0),
-          "mask_cols": lambda: mask.mask_cols(xs, 7, 0), "mask_rows": lambda: mask.mask_rows(xs, 7, 0)}[name]
+          "mask_cols": lambda: mask.mask_cols(xs, 7, 0), "mask_rows": lambda: mask.mask_rows(xs, 7, 0),
+          "dp_noise_elementwise": lambda: mask.dp_noise(xs, 7, 0, 0, 1.0, 256.0),
+          "dp_noise_gaussian": lambda: mask.dp_noise(xs, 7, 0, 1, 1.1, 256.0)}[name]
     fn()
     reps, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < 2.0:

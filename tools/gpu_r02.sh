@@ -44,6 +44,9 @@ run() {
                 python -u tools/matmul_sweep.py --families 16,32 0 1 2 4 8 >> gpurun_out/matmul_var.jsonl \
                 2>> gpurun_out/matmul_var.err || return 1
             done ;;
+    mask)   timeout -k 10 300 python -u tools/bench_mask.py > gpurun_out/bench_mask.jsonl 2> gpurun_out/bench_mask.err ;;
+    profmask) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_mask -o run --output-format csv \
+              -- python3 tools/bench_mask.py --steps 20 --no-cpu-baseline > gpurun_out/prof_mask.log 2>&1 ;;
     plfam)  timeout -k 10 600 python -u tools/sweep_pl_family.py > gpurun_out/sweep_pl_family.jsonl 2> gpurun_out/sweep_pl_family.err ;;
     profp)  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_p -o run --output-format csv \
               -- python3 bench.py --stage p --no-cpu-baseline > gpurun_out/prof_p.log 2>&1 ;;
