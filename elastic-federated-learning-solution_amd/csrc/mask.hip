@@ -18,6 +18,8 @@
 //
 // Every kernel is one streaming pass: read x once, write each output once. One lane owns four
 // consecutive elements (one Philox block, dwordx4 loads and stores). HBM-bound, no LDS, no MFMA.
+#include <cmath>
+
 #include "common.h"
 #include "pl_common.h"
 
@@ -232,13 +234,15 @@ __device__ __forceinline__ void normal4(uint64_t seed, uint64_t blk, float (&z)[
 // MODE 0, ElementWiseGaussianSumQuery.add_noise (dp_optimizer.py:70-71): v + normal * v * sigma;
 // MODE 1, GaussianSumQuery (tensorflow_privacy 0.3.0, TF 1.x branch): v + (normal * stddev + 0);
 // then safe_normalize (dp_optimizer.py:210-214): / num_microbatches. Each op rounds on its own.
-template <int MODE>
+// POW2: the divisor is a power of two and `div` holds its reciprocal: x * 2^-k is the correctly
+// rounded x / 2^k (the same exact real, one rounding), without the IEEE division sequence.
+template <int MODE, bool POW2>
 __device__ __forceinline__ float dp_one(float v, float z, float sigma, float div) {
   const float n = MODE == 0 ? (z * v) * sigma : z * sigma + 0.0f;
-  return (v + n) / div;
+  return POW2 ? (v + n) * div : (v + n) / div;
 }
 
-template <int MODE>
+template <int MODE, bool POW2>
 __global__ __launch_bounds__(kBlock) void k_dp_noise(const float* x, float* o,   // in place allowed
                                                      long long n, uint64_t seed, uint64_t ctr0, float sigma,
                                                      float div) {
@@ -251,10 +255,10 @@ __global__ __launch_bounds__(kBlock) void k_dp_noise(const float* x, float* o,  
     const f4 v = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + g);
     f4 r;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) r[j] = dp_one<MODE>(v[j], z[j], sigma, div);
+    for (int j = 0; j < 4; ++j) r[j] = dp_one<MODE, POW2>(v[j], z[j], sigma, div);
     stv(reinterpret_cast<f4*>(o) + g, r);
   } else {
-    for (int j = 0; j < 4 && i0 + j < n; ++j) o[i0 + j] = dp_one<MODE>(x[i0 + j], z[j], sigma, div);
+    for (int j = 0; j < 4 && i0 + j < n; ++j) o[i0 + j] = dp_one<MODE, POW2>(x[i0 + j], z[j], sigma, div);
   }
 }
 
@@ -335,7 +339,14 @@ EFL_API int efl_dp_noise(const float* x, float* out, int64_t n, int mode, float 
   const long long lanes = (n + 3) / 4;
   if (!lanes_ok(lanes)) { set_error("efl_dp_noise: tensor too large"); return EFL_E_INVALID_ARGUMENT; }
   hipStream_t s = (hipStream_t)stream;
-  if (mode == 0) k_dp_noise<0><<<grid_for(lanes), kBlock, 0, s>>>(x, out, n, seed, ctr0, sigma, divisor);
-  else k_dp_noise<1><<<grid_for(lanes), kBlock, 0, s>>>(x, out, n, seed, ctr0, sigma, divisor);
+  int ex = 0;
+  const bool pow2 = std::isfinite(divisor) && std::frexp(std::fabs(divisor), &ex) == 0.5f &&
+                    std::isnormal(1.0f / divisor);
+  const float d = pow2 ? 1.0f / divisor : divisor;   // exact for a power of two with a normal reciprocal
+  const unsigned grid = grid_for(lanes);
+  if (mode == 0 && pow2) k_dp_noise<0, true><<<grid, kBlock, 0, s>>>(x, out, n, seed, ctr0, sigma, d);
+  else if (mode == 0) k_dp_noise<0, false><<<grid, kBlock, 0, s>>>(x, out, n, seed, ctr0, sigma, d);
+  else if (pow2) k_dp_noise<1, true><<<grid, kBlock, 0, s>>>(x, out, n, seed, ctr0, sigma, d);
+  else k_dp_noise<1, false><<<grid, kBlock, 0, s>>>(x, out, n, seed, ctr0, sigma, d);
   return hip_status(hipGetLastError(), "efl_dp_noise");
 }

@@ -52,7 +52,8 @@ def test_normals_clamp(dp):
     assert abs(np.hypot(z[2], z[3]) - np.sqrt(-2 * np.log(np.float32(1e-7)))) < 1e-4
 
 
-@pytest.mark.parametrize("mode,sigma,div", [(0, 1.0, 1.0), (0, 0.7, 256.0), (1, 1.5, 3.0), (1, 0.0, 1.0)])
+@pytest.mark.parametrize("mode,sigma,div", [(0, 1.0, 1.0), (0, 0.7, 256.0), (1, 1.5, 3.0), (1, 0.0, 1.0),
+                                            (0, 1.1, 3.0), (1, 1.1, 256.0), (0, 1.0, -0.5), (1, 1.0, 2.0 ** 120)])
 @pytest.mark.parametrize("n", [5, 1000, 65539])
 def test_noise_bit_exact_given_normals(dp, mode, sigma, div, n):
     from efl.privacy.secret_sharing import NoiseStream
@@ -71,7 +72,7 @@ def test_noise_bit_exact_given_normals(dp, mode, sigma, div, n):
     ref = mask.dp_noise(x, 5, 40, mode, sigma, div)
     zr = mask.normal(5, 40, n)
     fin = np.isfinite(ref)
-    scale = (np.abs(x.astype(np.float64)) if mode == 0 else 1.0) * sigma * np.abs(zr) / div
+    scale = (np.abs(x.astype(np.float64)) if mode == 0 else 1.0) * sigma * np.abs(zr) / abs(div)
     bound = scale * ULP_TOL * 2.0 ** -23 + 2 * np.spacing(np.abs(ref).astype(np.float32)).astype(np.float64)
     err = np.abs(got.astype(np.float64) - ref.astype(np.float64))
     assert (err[fin] <= bound[fin]).all()
