@@ -687,7 +687,8 @@ def main():
         "d2d_copy_GBs": round(copy_gbs, 1) if copy_gbs else None,
         "seed_broadcast_us": round(bcast_us, 2),
         "backend": backend if world > 1 else None,
-        "devices_used": torch.cuda.device_count() if world == 1 else min(world, torch.cuda.device_count()),
+        "devices_used": 1 if world == 1 else min(world, torch.cuda.device_count()),
+        "devices_visible": torch.cuda.device_count(),
         "library": efl.lib.version(),
         "cpu_baseline": None,
     }

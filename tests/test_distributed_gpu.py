@@ -120,3 +120,36 @@ def test_two_ranks_share_cuda0_bit_identical():
     assert cg == whole.tensor.to_hex().strings()
     assert [p["counter"] for p in parts] == [parts[0]["pe"], N_P]
     assert torch.equal(kp1.decrypt(efl.HexTensor.from_strings(cg), dtype=torch.int64).cpu(), m)
+
+
+def _rccl_worker(rank, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    import torch.distributed as dist
+    from efl import distributed as edist
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    seed, pk = edist.broadcast_key_material(b"\x01" * 32, {"n": "ab", "hs": "cd"})
+    mx = edist.all_reduce_max([1.5, -2.5, 3.0])
+    dist.barrier()
+    q.put((seed, pk, mx, dist.get_backend()))
+    dist.destroy_process_group()
+
+
+def test_rccl_collectives_of_the_multi_gpu_path():
+    """The collectives bench.py and efl.distributed run over RCCL on an 8-GPU node (key material
+    broadcast, max over ranks, barrier) exercised on this box's one GPU in a single-rank RCCL group:
+    the same device placement of the tensors (_device_for) and the same communicator setup."""
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    q = tmp.get_context("spawn").Queue()
+    procs = tmp.start_processes(_rccl_worker, args=(port, q), nprocs=1, join=False, start_method="spawn")
+    try:
+        seed, pk, mx, backend = q.get(timeout=100)
+    except Exception:
+        procs.join(timeout=5)
+        raise
+    while not procs.join(timeout=30):
+        pass
+    assert backend == "nccl" and seed == b"\x01" * 32 and pk == {"n": "ab", "hs": "cd"}
+    assert mx == [1.5, -2.5, 3.0]
