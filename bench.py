@@ -442,7 +442,7 @@ def stage_p_matmul(args, efl, pc, kp, lib, sh, stream, dev):
             S *= 2
     else:
         waves = 2 if fam >= 32 else 4                    # k_matmul28's waves per SIMD
-        while 2 * S <= 8 and 2 * S <= v and u * w * G * S < 256 * 4 * 64 * 2 * waves:
+        while 2 * S <= 8 and 2 * S <= v and u * w * G * S < 256 * 4 * 64 * waves:
             S *= 2
     # x R and its odd powers (1 squaring + 2^(w-1) - 1 products); combining the partials + conversion out
     products = u * v * (1 + (1 << (MATMUL_WINDOW - 1))) + (2 * S * u * w if S > 1 else 0)

@@ -494,6 +494,111 @@ __global__ __launch_bounds__(256) void k_wmask(const long long* __restrict__ ym,
   wm[i] = mask;
 }
 
+// Multiply schedules of k_matmul28, built ahead by k_mmevents (round 2). Scanning every term at
+// every bit level inside k_matmul28 cost as much as the Montgomery products themselves: ~15 scan
+// steps per event on the MNIST product, each a handful of dependent cached loads, and the wave
+// waits for its slowest group (tools/matmul_probe.py, EFL_MAT_PROBE=1: the kernel without its
+// products still took half its time). Here one lane per (output, split) runs that scan once and
+// writes the multiplies in the order the product consumes them (bit level descending, terms
+// ascending within a level) as 32-bit words: bits [0,16) j - j0, [16,21) odd-power entry, [21]
+// negative term, [22,32) level. Word e of list l is at EV[e * NL + l] (a wave's lists side by side,
+// so k_matmul28's per-event reads are coalesced). hdr[l] = {events, top level}; -1 events: the list
+// does not fit (more than `cap` events, a level past 1023, a split wider than 2^16 terms) and
+// k_matmul28 scans that output's terms itself as before. mnv[l] = the output's minimum exponent.
+constexpr int kEvLevelShift = 22, kEvNegBit = 21;
+constexpr long long kEvLevels = 1ll << (32 - kEvLevelShift);
+static_assert(kMatWin <= 6, "odd-power entry must fit the event word's 5 bits");
+
+// Levels below kEvHistLevels are sorted by a per-lane counting sort in LDS (two passes over the
+// terms: count events per level, then place each at its level's next slot — the same order as the
+// level-major scan, which stays as the path for higher levels).
+constexpr int kEvBlock = 128, kEvHistLevels = 128;
+
+__device__ __forceinline__ uint32_t ev_word(int jr, uint64_t ay, long long y, long long p, long long b) {
+  const uint32_t ent = (uint32_t)(((ay >> p) & ((1ull << kMatWin) - 1ull)) >> 1);
+  return (uint32_t)jr | (ent << 16) | ((y < 0 ? 1u : 0u) << kEvNegBit) | ((uint32_t)b << kEvLevelShift);
+}
+
+__global__ __launch_bounds__(kEvBlock) void k_mmevents(const long long* __restrict__ xe,
+                                                       const long long* __restrict__ ym,
+                                                       const long long* __restrict__ ye,
+                                                       const unsigned long long* __restrict__ wmask, int u, int v,
+                                                       int w, int S, int cap, uint32_t* __restrict__ EV,
+                                                       int2* __restrict__ hdr, long long* __restrict__ mnv) {
+  __shared__ uint32_t hist[kEvHistLevels * kEvBlock];   // level-major, lane-minor: conflict-free
+  const long long UW = (long long)u * w, NL = UW * S;
+  const long long l = (long long)blockIdx.x * kEvBlock + threadIdx.x;
+  if (l >= NL) return;
+  const int sp = (int)(l / UW);
+  const int row = (int)(l % UW % u), kk = (int)(l % UW / u);
+  const long long* xr = xe + (long long)row * v;
+  const long long* yc = ym + kk;
+  const long long* ec = ye + kk;
+  const unsigned long long* wc = wmask + kk;
+  long long mn = 0x7FFFFFFFFFFFFFFFll;
+  for (int j = 0; j < v; ++j) {
+    const long long ex = xr[j] + ec[(long long)j * w];
+    mn = ex < mn ? ex : mn;
+  }
+  mnv[l] = mn;
+  const int j0 = (int)((long long)v * sp / S), j1 = (int)((long long)v * (sp + 1) / S);
+  long long top = 0;
+  for (int j = j0; j < j1; ++j) {
+    const long long y = yc[(long long)j * w];
+    if (y == 0) continue;
+    const uint64_t ay = y < 0 ? 0ull - (uint64_t)y : (uint64_t)y;
+    const long long lvl = xr[j] + ec[(long long)j * w] - mn + (64 - __clzll((long long)ay));
+    top = lvl > top ? lvl : top;
+  }
+  int cnt = 0;
+  bool ok = j1 - j0 <= 65536 && top <= kEvLevels;
+  if (ok && top <= kEvHistLevels) {
+    uint32_t* H = hist + threadIdx.x;
+    for (int lv = 0; lv < (int)top; ++lv) H[lv * kEvBlock] = 0;
+    for (int j = j0; j < j1; ++j) {
+      const int d = (int)(xr[j] + ec[(long long)j * w] - mn);
+      for (unsigned long long m = wc[(long long)j * w]; m; m &= m - 1) H[(d + __ffsll((long long)m) - 1) * kEvBlock]++;
+    }
+    uint32_t run = 0;   // exclusive offsets, top level first
+    for (int lv = (int)top - 1; lv >= 0; --lv) {
+      const uint32_t c = H[lv * kEvBlock];
+      H[lv * kEvBlock] = run;
+      run += c;
+    }
+    ok = run <= (uint32_t)cap;
+    if (ok) {
+      cnt = (int)run;
+      for (int j = j0; j < j1; ++j) {
+        const long long y = yc[(long long)j * w];
+        const uint64_t ay = y < 0 ? 0ull - (uint64_t)y : (uint64_t)y;
+        const int d = (int)(xr[j] + ec[(long long)j * w] - mn);
+        for (unsigned long long m = wc[(long long)j * w]; m; m &= m - 1) {
+          const int p = __ffsll((long long)m) - 1;
+          const uint32_t pos = H[(d + p) * kEvBlock]++;
+          EV[(long long)pos * NL + l] = ev_word(j - j0, ay, y, p, d + p);
+        }
+      }
+    }
+  } else {
+    for (long long b = top - 1; ok && b >= 0; --b) {
+      for (int j = j0; j < j1; ++j) {
+        const long long p = b - (xr[j] + ec[(long long)j * w] - mn);
+        if (p >= 0 && p < 64 && ((wc[(long long)j * w] >> p) & 1ull)) {
+          if (cnt == cap) {
+            ok = false;
+            break;
+          }
+          const long long y = yc[(long long)j * w];
+          const uint64_t ay = y < 0 ? 0ull - (uint64_t)y : (uint64_t)y;
+          EV[(long long)cnt * NL + l] = ev_word(j - j0, ay, y, p, b);
+          ++cnt;
+        }
+      }
+    }
+  }
+  hdr[l] = make_int2(ok ? cnt : -1, ok ? (int)top : 0);
+}
+
 // x R mod n^2 and its odd powers (radix 2^28, Montgomery) for every x element:
 // entry e of element i at Xm + (i * kMatEntries + e) * (CP * G), lane g's slice at + g * CP
 template <int C, int G>
@@ -544,13 +649,14 @@ __global__ __launch_bounds__(kSlBlock, C >= 32 ? EFL_MAT_WAVES32 : EFL_MAT_WAVES
     Key k, const uint32_t* __restrict__ Xm, const long long* __restrict__ xe, const long long* __restrict__ ym,
     const long long* __restrict__ ye, uint32_t* __restrict__ zpos, uint32_t* __restrict__ zneg,
     long long* __restrict__ ze, int u, int v, int w, int S, uint32_t* __restrict__ P,
-    const unsigned long long* __restrict__ wmask) {
+    const unsigned long long* __restrict__ wmask, const uint32_t* __restrict__ EV, const int2* __restrict__ hdr,
+    const long long* __restrict__ mnv) {
   constexpr int L = C * G, E = kSlBlock / G;
   constexpr int C28 = s28::limbs_per_lane(L, G), L28 = C28 * G, CP = pad4<C28>();
   extern __shared__ uint32_t lds[];
   SL_ELEMENT(E, G)
-  const long long UW = (long long)u * w;
-  if (i >= UW * S) return;
+  const long long UW = (long long)u * w, NL = UW * S;
+  if (i >= NL) return;
   const int sp = (int)(i / UW);                      // split of the terms this group takes
   const int row = (int)(i % UW % u), kk = (int)(i % UW / u);
   const long long o = (long long)row * w + kk;
@@ -562,20 +668,21 @@ __global__ __launch_bounds__(kSlBlock, C >= 32 ? EFL_MAT_WAVES32 : EFL_MAT_WAVES
   const long long* yc = ym + kk;
   const long long* ec = ye + kk;
   const unsigned long long* wc = wmask + kk;
-  long long mn = 0x7FFFFFFFFFFFFFFFll;
-  for (int j = 0; j < v; ++j) {
-    const long long ex = xr[j] + ec[(long long)j * w];
-    mn = ex < mn ? ex : mn;
-  }
+  const long long mn = mnv[i];                       // min over j of xe_ij + ye_jk (k_mmevents)
   // this split's terms [j0, j1); top bit level of any of their exponents |y| 2^d
   const int j0 = (int)((long long)v * sp / S), j1 = (int)((long long)v * (sp + 1) / S);
-  long long top = 0;
-  for (int j = j0; j < j1; ++j) {
-    const long long y = yc[(long long)j * w];
-    if (y == 0) continue;
-    const uint64_t ay = y < 0 ? 0ull - (uint64_t)y : (uint64_t)y;
-    const long long lvl = xr[j] + ec[(long long)j * w] - mn + (64 - __clzll((long long)ay));
-    top = lvl > top ? lvl : top;
+  const int2 h = hdr[i];
+  const bool listed = h.x >= 0;                      // k_mmevents wrote this group's multiplies
+  long long top = h.y;
+  if (!listed) {
+    top = 0;
+    for (int j = j0; j < j1; ++j) {
+      const long long y = yc[(long long)j * w];
+      if (y == 0) continue;
+      const uint64_t ay = y < 0 ? 0ull - (uint64_t)y : (uint64_t)y;
+      const long long lvl = xr[j] + ec[(long long)j * w] - mn + (64 - __clzll((long long)ay));
+      top = lvl > top ? lvl : top;
+    }
   }
   // Each group walks its own event list: per bit level from the top, a squaring of each started
   // product, then one multiply per term with a window starting at that level (by the term's odd
@@ -585,6 +692,9 @@ __global__ __launch_bounds__(kSlBlock, C >= 32 ? EFL_MAT_WAVES32 : EFL_MAT_WAVES
   bool started0 = false, started1 = false;   // products still 1 take their first term as a copy
   long long b = top - 1;
   int j = 0, phase = 0;                      // phase 0: square POS, 1: square NEG, 2: terms
+  // listed groups: the next multiply word, read one event ahead (it arrives while a product runs)
+  int ev_i = 0;
+  uint32_t ev = listed && h.x > 0 ? EV[i] : 0u;
   // The next event of this group's list: op 0/1 square POS/NEG, 2/3 multiply x_j^v into POS/NEG,
   // -1 at the end; `addr` = the multiply's operand in Xm, `copy` = it is its product's first term
   // (a product counts as started once its first multiply has been scanned).
@@ -599,6 +709,24 @@ __global__ __launch_bounds__(kSlBlock, C >= 32 ? EFL_MAT_WAVES32 : EFL_MAT_WAVES
         phase = 2;
         j = j0;
         if (started1) op = 1;
+      } else if (listed) {
+        if (ev_i < h.x && (long long)(ev >> kEvLevelShift) == b) {
+          const int ent = (int)((ev >> 16) & 31u);
+          addr = (((long long)row * v + j0 + (int)(ev & 0xFFFFu)) * kMatEntries + ent) * (CP * G) + g * CP;
+          if ((ev >> kEvNegBit) & 1u) {
+            op = 3;
+            copy = !started1;
+            started1 = true;
+          } else {
+            op = 2;
+            copy = !started0;
+            started0 = true;
+          }
+          if (++ev_i < h.x) ev = EV[(long long)ev_i * NL + i];
+        } else {
+          --b;
+          phase = 0;
+        }
       } else if (j >= j1) {
         --b;
         phase = 0;
@@ -660,9 +788,15 @@ __global__ __launch_bounds__(kSlBlock, C >= 32 ? EFL_MAT_WAVES32 : EFL_MAT_WAVES
     if (op < 0) break;
     uint32_t* acc = (op & 1) ? ACC[1] : ACC[0];
     if (op < 2) from_lds<C28>(t, acc, E, g);
+#if EFL_MAT_PROBE == 2   // timing probe (wrong results): every multiply operand from one cached slot
+    else load28<C28>(t, Xm + g * CP);
+#else
     else load28<C28>(t, Xm + addr);
+#endif
     if (!copy) {
+#if EFL_MAT_PROBE != 1   // timing probe (wrong results): EFL_MAT_PROBE=1 skips the products
       s28::mont_mul<C28, G>(t, LdsElem{acc, E}, m28, minv28, g);
+#endif
       lds_sync();
     }
     to_lds<C28>(acc, E, g, t);
@@ -1075,31 +1209,49 @@ hipError_t run_matmul28(const Key& k, const uint32_t* X, const long long* xe, co
                         uint32_t* zpos, uint32_t* zneg, long long* ze, int u, int v, int w, hipStream_t s) {
   constexpr int C28 = s28::limbs_per_lane(C * G, G), L28 = C28 * G, E = kSlBlock / G;
   const long long nx = (long long)u * v, UW = (long long)u * w;
-  // terms split S ways over separate groups when one group per output would give fewer than two
-  // rounds of the kernel's waves per SIMD (a second round evens out the groups' unequal event
-  // counts; more splits repeat each split's squarings: 1034 / 1133 / 1324 products per output of
-  // the MNIST product at S = 2 / 4 / 8, profiles/r02/matmul_splits.jsonl); partials combined after.
+  // terms split S ways over separate groups when one group per output would leave part of one
+  // round of the kernel's waves per SIMD empty; every split repeats the squarings (982 / 1034 / 1133
+  // products per output of the MNIST product at S = 1 / 2 / 4), and the partials are combined
+  // after. Round 1 and the scan-per-event kernel wanted two rounds (S = 4 there) to even out the
+  // groups' scan lengths; with the event lists (k_mmevents) one round is faster: 17.0 ms at S = 2
+  // against 18.1 at S = 4 and 29.2 at S = 1 (profiles/r02/matmul_splits_events.jsonl).
   // bench.py mirrors this choice.
-  constexpr long long kTwoRounds = 256ll * 4 * 64 * 2 * (C >= 32 ? EFL_MAT_WAVES32 : EFL_MAT_WAVES16);
+  constexpr long long kOneRound = 256ll * 4 * 64 * (C >= 32 ? EFL_MAT_WAVES32 : EFL_MAT_WAVES16);
   int S = 1;
   const int fixed = g_mat_splits.load();
   if (fixed > 0) {
     while (2 * S <= fixed && 2 * S <= v) S *= 2;
   } else {
-    while (2 * S <= 8 && 2 * S <= v && UW * G * S < kTwoRounds) S *= 2;
+    while (2 * S <= 8 && 2 * S <= v && UW * G * S < kOneRound) S *= 2;
   }
   const size_t slot = (size_t)pad4<C28>() * G;
+  // event-list capacity per (output, split): five windows per term cover 24-bit mantissas (the
+  // fp32 encode's), three the decrease_precision weights; a list past it falls back to the scan
+  const long long NL = UW * S, terms = (v + S - 1) / S;
+  const int cap = (int)(terms * 5 < 4096 ? terms * 5 : 4096);
   // stream-ordered scratch: the odd powers of every x (kMatEntries padded radix-2^28 slices each),
-  // then the S > 1 partials, then the window masks of y
+  // then the S > 1 partials, the event lists, then (8-byte aligned) the window masks of y, the list
+  // headers and the outputs' minimum exponents
   const size_t x_words = (size_t)nx * kMatEntries * slot, p_words = S > 1 ? (size_t)S * UW * 2 * slot : 0;
+  const size_t ev_words = ((size_t)NL * cap + 1) & ~(size_t)1;
   const size_t yw = (size_t)v * w;
   uint32_t* Xm = nullptr;
-  hipError_t err = hipMallocAsync(reinterpret_cast<void**>(&Xm), (x_words + p_words) * 4 + yw * 8, s);
+  hipError_t err = hipMallocAsync(reinterpret_cast<void**>(&Xm),
+                                  (x_words + p_words + ev_words) * 4 + yw * 8 + (size_t)NL * 16, s);
   if (err != hipSuccess) return err;
   uint32_t* P = S > 1 ? Xm + x_words : nullptr;
-  unsigned long long* wm = reinterpret_cast<unsigned long long*>(Xm + x_words + p_words);
+  uint32_t* EV = Xm + x_words + p_words;
+  unsigned long long* wm = reinterpret_cast<unsigned long long*>(EV + ev_words);
+  int2* hdr = reinterpret_cast<int2*>(wm + yw);
+  long long* mnv = reinterpret_cast<long long*>(hdr + NL);
   hipLaunchKernelGGL(k_wmask, dim3((unsigned)((yw + 255) / 256)), dim3(256), 0, s, ym, wm, (long long)yw);
   err = hipGetLastError();
+  if (err == hipSuccess) {
+    hipLaunchKernelGGL(k_mmevents, dim3((unsigned)((NL + kEvBlock - 1) / kEvBlock)), dim3(kEvBlock), 0, s, xe, ym, ye,
+                       wm, u, v, w, S,
+                       cap, EV, hdr, mnv);
+    err = hipGetLastError();
+  }
   if (err == hipSuccess) {
     hipLaunchKernelGGL((k_tomont28<C, G>), dim3(grid_of(nx, G)), dim3(kSlBlock), (size_t)2 * L28 * E * 4, s, k, X, Xm,
                        nx);
@@ -1107,7 +1259,7 @@ hipError_t run_matmul28(const Key& k, const uint32_t* X, const long long* xe, co
   }
   if (err == hipSuccess) {
     hipLaunchKernelGGL((k_matmul28<C, G>), dim3(grid_of(UW * S, G)), dim3(kSlBlock), (size_t)2 * L28 * E * 4, s, k,
-                       Xm, xe, ym, ye, zpos, zneg, ze, u, v, w, S, P, wm);
+                       Xm, xe, ym, ye, zpos, zneg, ze, u, v, w, S, P, wm, EV, hdr, mnv);
     err = hipGetLastError();
   }
   if (err == hipSuccess && S > 1) {

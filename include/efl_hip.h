@@ -237,8 +237,10 @@ int efl_pl_invert(const void* key_block, const efl_pl_key* key, const uint32_t* 
  * y_mantissa / y_exponent [v][w] int64. For each output z_exponent = min_j(xe + ye) and the terms
  * (x^|y|)^(2^(xe + ye - min)) are multiplied into z_pos (y > 0) or z_neg (y < 0); the caller
  * finishes z = z_pos * z_neg^-1 (efl_pl_invert + efl_pl_add). With the radix-2^28 family the
- * kernel first writes x R mod n^2 for every x into u*v*L28*4 bytes of scratch taken and released
- * on `stream` (hipMallocAsync / hipFreeAsync); a failed allocation returns the HIP error. */
+ * kernels first write x R mod n^2 and its odd powers for every x (u*v*16 padded radix-2^28
+ * numbers), then every output's multiply schedule (u*w*S lists of up to 5*ceil(v/S) 32-bit words,
+ * S the term split) into scratch taken and released on `stream` (hipMallocAsync / hipFreeAsync);
+ * a failed allocation returns the HIP error. */
 int efl_pl_matmul(const void* key_block, const efl_pl_key* key, const uint32_t* x_mantissa,
                   const int64_t* x_exponent, const int64_t* y_mantissa, const int64_t* y_exponent,
                   uint32_t* z_pos, uint32_t* z_neg, int64_t* z_exponent, int u, int v, int w,
