@@ -1226,9 +1226,11 @@ hipError_t run_matmul28(const Key& k, const uint32_t* X, const long long* xe, co
   }
   const size_t slot = (size_t)pad4<C28>() * G;
   // event-list capacity per (output, split): five windows per term cover 24-bit mantissas (the
-  // fp32 encode's), three the decrease_precision weights; a list past it falls back to the scan
+  // fp32 encode's), three the decrease_precision weights; a list past it falls back to the scan.
+  // The lists take at most 1 GiB: larger products get shorter lists (more outputs scan).
   const long long NL = UW * S, terms = (v + S - 1) / S;
-  const int cap = (int)(terms * 5 < 4096 ? terms * 5 : 4096);
+  long long cap = terms * 5 < 4096 ? terms * 5 : 4096;
+  if (cap * NL > (1ll << 28)) cap = (1ll << 28) / NL;
   // stream-ordered scratch: the odd powers of every x (kMatEntries padded radix-2^28 slices each),
   // then the S > 1 partials, the event lists, then (8-byte aligned) the window masks of y, the list
   // headers and the outputs' minimum exponents
@@ -1249,7 +1251,7 @@ hipError_t run_matmul28(const Key& k, const uint32_t* X, const long long* xe, co
   if (err == hipSuccess) {
     hipLaunchKernelGGL(k_mmevents, dim3((unsigned)((NL + kEvBlock - 1) / kEvBlock)), dim3(kEvBlock), 0, s, xe, ym, ye,
                        wm, u, v, w, S,
-                       cap, EV, hdr, mnv);
+                       (int)cap, EV, hdr, mnv);
     err = hipGetLastError();
   }
   if (err == hipSuccess) {

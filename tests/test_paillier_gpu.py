@@ -392,6 +392,53 @@ def _matmul_vs_oracle(efl):
     assert dec == want
 
 
+def _matmul_case(efl, xe, ym, ye, seed):
+    k = ENC_KEYS[0]
+    kp = keypair(efl, k)
+    okp = P.Keypair(int(k["n"], 16), int(k["hs"], 16), k["a_bits"] // 8, 1, int(k["p"], 16), int(k["q"], 16))
+    u, v = xe.shape
+    xm_plain = np.random.default_rng(seed).integers(-2**20, 2**20, (u, v))
+    ct = kp.encrypt(torch.from_numpy(xm_plain))
+    zm, ze = kp.matmul(ct.tensor, torch.from_numpy(xe), torch.from_numpy(ym), torch.from_numpy(ye))
+    xs = [[int(s, 16) for s in row] for row in np.array(ct.tensor.to_hex().strings()).reshape(u, v)]
+    om, oe = P.matmul(okp, xs, xe.tolist(), ym.tolist(), ye.tolist())
+    assert np.array_equal(ze.cpu().numpy(), np.array(oe))
+    assert zm.to_hex().to_ints() == [c for row in om for c in row]
+
+
+@pytest.mark.parametrize("case", ["sorted", "level_scan", "over_capacity", "deep", "mixed"])
+@pytest.mark.parametrize("splits", [0, 1])
+@pytest.mark.parametrize("c", [16, 32])
+def test_matmul_schedule_paths(efl, case, splits, c):
+    """Every path of the multiply schedules (k_mmevents / k_matmul28) equals the oracle: the LDS
+    counting sort (levels < 128), the builder's level-major scan (levels 128..1023), and the
+    in-kernel scan for lists that do not fit — more than 5 windows per term (60-bit weights) or a
+    level past 1023 — alone and next to listed outputs in the same wave ("mixed": one row's
+    exponents spread past 1023)."""
+    rng = np.random.default_rng(21)
+    u, v, w = 3, 5, 4
+    xe = rng.integers(-30, -10, (u, v))
+    ye = rng.integers(-25, -12, (v, w))
+    ym = rng.integers(-2**11, 2**11, (v, w))
+    if case == "level_scan":
+        xe[:, 0] -= 300
+    elif case == "over_capacity":
+        ym = rng.integers(-2**60, 2**60, (v, w))
+    elif case == "deep":
+        xe[:, 1] -= 1100
+    elif case == "mixed":
+        xe[1, 2] -= 1100
+        ym[:, 1] = rng.integers(-2**60, 2**60, v)
+    lib = efl.lib.raw()
+    ln = ENC_KEYS[0]["n_bytes"] // 4
+    prev = lib.efl_pl_tune(ln, 3, splits)
+    try:
+        with family(ln, False, c):
+            _matmul_case(efl, xe, ym, ye, 3)
+    finally:
+        lib.efl_pl_tune(ln, 3, prev)
+
+
 @pytest.mark.parametrize("splits", [1, 2, 3, 4, 16])
 def test_matmul_term_splits(efl, splits):
     """efl_pl_tune(ln, 3, S) fixes k_matmul28's term splits (rounded down to a power of two, at
