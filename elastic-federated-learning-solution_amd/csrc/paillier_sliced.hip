@@ -224,15 +224,13 @@ __global__ __launch_bounds__(kSlBlock) SL_OCC void k_fbpowm(Key k, const uint32_
 // hs^(a') mod n^2 through the radix-2^28 table (same lookup order as fbpowm_mont), result in
 // NORMAL form as this lane's C 32-bit words. Scratch: B (entry / conversion, L28 words per element).
 template <int C, int G>
-__device__ __forceinline__ void fbpowm28(uint32_t (&out)[C], const Key& k, uint32_t* A, uint32_t* B, int E,
-                                         int words, int g) {
+__device__ __forceinline__ void fbpowm28_walk(uint32_t (&acc)[s28::limbs_per_lane(C * G, G)], const Key& k,
+                                              uint32_t* A, uint32_t* B, int E, int words,
+                                              const uint32_t (&m28)[s28::limbs_per_lane(C * G, G)], int g) {
   constexpr int L = C * G;
   constexpr int C28 = s28::limbs_per_lane(L, G), L28 = C28 * G;
   const int size = regroup_shared(A, E, words, k.d.group_size, g);
   const int W = table_window(k.d);
-  uint32_t m28[C28], acc[C28];
-  slice_uniform<C28>(m28, k.at(k.d.off_n2_28), g);
-  slice_uniform<C28>(acc, k.at(k.d.off_n2_one28), g);
   const uint32_t minv28 = k.d.n2_minv28;
   const uint32_t* table = k.at(k.d.off_table28);
   const int cols = k.d.table_cols;
@@ -247,41 +245,24 @@ __device__ __forceinline__ void fbpowm28(uint32_t (&out)[C], const Key& k, uint3
       lds_sync();
     }
   }
-  s28::mont_mul<C28, G>(acc, Unit{}, m28, minv28, g);   // hs^(a') mod n^2 (< n^2)
+}
+
+// hs^(a') mod n^2 through the radix-2^28 table (gmp_utils.cc:107-144), as 32-bit words
+template <int C, int G>
+__device__ __forceinline__ void fbpowm28(uint32_t (&out)[C], const Key& k, uint32_t* A, uint32_t* B, int E,
+                                         int words, int g) {
+  constexpr int L = C * G;
+  constexpr int C28 = s28::limbs_per_lane(L, G), L28 = C28 * G;
+  uint32_t m28[C28], acc[C28];
+  slice_uniform<C28>(m28, k.at(k.d.off_n2_28), g);
+  slice_uniform<C28>(acc, k.at(k.d.off_n2_one28), g);
+  fbpowm28_walk<C, G>(acc, k, A, B, E, words, m28, g);
+  s28::mont_mul<C28, G>(acc, Unit{}, m28, k.d.n2_minv28, g);   // hs^(a') mod n^2 (< n^2)
   lds_sync();
   to_lds<C28>(B, E, g, acc);
   lds_sync();
   s28::to_words<C>(out, B, E, L28, g);
   lds_sync();
-}
-
-// PaillierEncrypt with fresh randomness through the radix-2^28 table: c = g(m) * hs^(a') mod n^2
-template <int C, int G>
-__global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_encrypt28(Key k, const long long* __restrict__ m,
-                                                                          uint32_t* __restrict__ out, long long N,
-                                                                          uint64_t seed, long long ctr0) {
-  constexpr int L = C * G, E = kSlBlock / G;
-  constexpr int L28 = s28::limbs_per_lane(L, G) * G;
-  extern __shared__ uint32_t lds[];
-  SL_ELEMENT(E, G)
-  if (i >= N) return;
-  const int words = (k.d.a_bits + 31) >> 5;
-  uint32_t* B = lds + e;
-  uint32_t* A = lds + L28 * E + e;
-  draw_a<G>(A, E, words, k.d.a_bits, seed, (uint64_t)(ctr0 + i), g);
-  lds_sync();
-  uint32_t h[C];
-  fbpowm28<C, G>(h, k, A, B, E, words, g);
-  asm volatile("" ::: "memory");
-  uint32_t n2[C], c[C];
-  slice_uniform<C>(n2, k.at(k.d.off_n2), g);
-  const uint32_t minv = k.d.n2_minv;
-  to_lds<C>(B, E, g, h);
-  make_g<C, G>(c, m[i], k, n2, g);
-  lds_sync();
-  mont_mul<C, G>(c, LdsElem{B, E}, n2, minv, g);                   // g hsa R^-1
-  mont_mul<C, G>(c, Uniform{k.at(k.d.off_n2_r2)}, n2, minv, g);   // g hsa
-  store_slice<C>(out + i * L, g, c);
 }
 
 template <int C, int G>
@@ -394,6 +375,49 @@ __device__ __forceinline__ void store_from_mont28(uint32_t* out, uint32_t (&t)[s
   uint32_t w[C];
   s28::to_words<C>(w, SCR, E, L28, g);
   store_slice<C>(out, g, w);
+}
+
+// PaillierEncrypt with fresh randomness through the radix-2^28 table: c = g(m) * hs^(a') mod n^2.
+// The walk starts from g(m) R instead of R, so it leaves c R and one conversion out gives c: one
+// radix-2^28 product (g -> g R) instead of round 1's two 32-bit-limb products after the walk, which
+// also spilled at C = 32. Same-box A/B (profiles/r02/ab_encrypt_tail.jsonl): 1024-bit n +7 %
+// encrypts/s; 4096-bit n 1.2-1.8 % slower, with the hot loop identical instruction for instruction
+// (tools/isa_loops.py) and only its code placement moved — keeping the round-1 tail there in the
+// same build measured slower still (-3 %).
+template <int C, int G>
+__global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_encrypt28(Key k, const long long* __restrict__ m,
+                                                                          uint32_t* __restrict__ out, long long N,
+                                                                          uint64_t seed, long long ctr0) {
+  constexpr int L = C * G, E = kSlBlock / G;
+  constexpr int C28 = s28::limbs_per_lane(L, G), L28 = C28 * G;
+  extern __shared__ uint32_t lds[];
+  SL_ELEMENT(E, G)
+  if (i >= N) return;
+  const int words = (k.d.a_bits + 31) >> 5;
+  uint32_t* B = lds + e;
+  uint32_t* A = lds + L28 * E + e;
+  uint32_t m28[C28], acc[C28];
+  {
+    uint32_t n2[C], c[C];
+    slice_uniform<C>(n2, k.at(k.d.off_n2), g);
+    make_g<C, G>(c, m[i], k, n2, g);
+    to_lds<C>(B, E, g, c);
+  }
+  lds_sync();
+  s28::from_words<C28>(acc, B, E, L, g);
+  lds_sync();
+  // R^2 as the LDS operand, like a table entry
+  slice_uniform<C28>(m28, k.at(k.d.off_n2_r2_28), g);
+  to_lds<C28>(B, E, g, m28);
+  slice_uniform<C28>(m28, k.at(k.d.off_n2_28), g);
+  lds_sync();
+  s28::mont_mul<C28, G>(acc, LdsElem{B, E}, m28, k.d.n2_minv28, g);   // g R
+  lds_sync();
+  draw_a<G>(A, E, words, k.d.a_bits, seed, (uint64_t)(ctr0 + i), g);
+  lds_sync();
+  fbpowm28_walk<C, G>(acc, k, A, B, E, words, m28, g);                 // g hs^(a') R
+  lds_sync();
+  store_from_mont28<C, G>(out + i * L, acc, m28, k.d.n2_minv28, B, E, g);
 }
 
 template <int C, int G>

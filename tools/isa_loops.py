@@ -16,9 +16,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 from test_isa_guard import LIB, OBJDUMP, backward_loops, code_objects, kernel_instructions, loop_mix  # noqa: E402,E501
 
-def kernel_lines(name):
+def kernel_lines(name, lib=LIB):
     texts = []
-    for blob in code_objects(LIB):
+    for blob in code_objects(lib):
         with tempfile.NamedTemporaryFile(suffix=".o") as f:
             f.write(blob)
             f.flush()
@@ -33,8 +33,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("kernel")
     ap.add_argument("--top", type=int, default=12)
+    ap.add_argument("--lib", default=LIB, help="library to disassemble (default: the built libefl_hip.so)")
     a = ap.parse_args()
-    ins = kernel_lines(a.kernel)
+    ins = kernel_lines(a.kernel, a.lib)
     for t, k in backward_loops(ins):
         mix = loop_mix(ins, (t, k))
         print(f"loop [{t}, {k}] {k + 1 - t} insns:", ", ".join(f"{o} {n}" for o, n in mix.most_common(a.top)))
