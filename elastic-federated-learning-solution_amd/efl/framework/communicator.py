@@ -32,6 +32,7 @@ import logging
 import os
 import threading
 import time
+import warnings
 from concurrent import futures
 
 import grpc
@@ -345,7 +346,10 @@ class Communicator(object):
         self._waiters[(name, step)] = w
         return None, w
 
-    def _recv_raw(self, name, dtype=None):
+    def _recv_raw(self, name, dtype=None, readonly=False):
+        """readonly=True (hooks that only read the payload, e.g. to copy it to the GPU): the
+        tensor is a view of the received message bytes instead of a private copy; it must not be
+        written to."""
         step = self.step
         log.debug("%s: waiting %s step %d", self._federal_role, name, step)
         deadline = time.monotonic() + self._timeout
@@ -371,7 +375,7 @@ class Communicator(object):
             p.finish(15, msg)   # DATA_LOSS to the sender
             raise errors.DataLossError(msg)
         try:
-            out = self._materialize(p.payload, dtype)
+            out = self._materialize(p.payload, dtype, readonly)
         except Exception as e:   # deserialize error -> Unknown to both sides (:241-246)
             p.finish(2, f"Tensor named {name} deserialize error.")
             raise errors.UnknownError(f"Tensor named {name} deserialize error: {e}") from None
@@ -379,15 +383,21 @@ class Communicator(object):
         return out
 
     @staticmethod
-    def _materialize(msg: wire.TensorMsg, dtype):
+    def _materialize(msg: wire.TensorMsg, dtype, readonly=False):
         from efl.privacy.hex_tensor import HexTensor
         if msg.dtype == wire.DT_STRING:
             if msg.content is not None and len(msg.content):
                 return HexTensor.from_tensor_content(bytes(msg.content), msg.shape)
             return HexTensor.from_strings(np.array(msg.typed, dtype=object).reshape(msg.shape))
         arr = msg.to_numpy()
-        t = torch.from_numpy(arr.copy() if not arr.flags.writeable else arr)
-        return t
+        if arr.flags.writeable:
+            return torch.from_numpy(arr)
+        if not readonly:
+            return torch.from_numpy(arr.copy())
+        # a view of the (immutable) message bytes: torch warns that it cannot mark it read-only
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore", UserWarning)
+            return torch.from_numpy(arr)
 
 
 class CommunicatorHook(object):

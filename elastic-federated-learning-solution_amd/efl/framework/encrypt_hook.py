@@ -50,6 +50,8 @@ class _PinnedPool:
 
 @exporter.export("privacy.FixedPointHook")
 class FixedPointHook(TensorHook):
+    readonly_recv = True   # post_recv reads the received payloads in place (False: private copies)
+
     def __init__(self, names=None, decrease_precision=False, return_device=None, encode=None,
                  decode=None, reuse_buffers=False, stats=None):
         """names: regex of logical tensor names to transform (default: every float tensor).
@@ -134,8 +136,9 @@ class FixedPointHook(TensorHook):
         if dt not in _FLOATS or not self._match(name):
             return None
         t = self._tick()
-        M = raw_recv(name + "_mantissa")
-        E = raw_recv(name + "_exponent")
+        # the payloads are only read (copied to the GPU): views of the message bytes, no host copy
+        M = raw_recv(name + "_mantissa", readonly=self.readonly_recv)
+        E = raw_recv(name + "_exponent", readonly=self.readonly_recv)
         t = self._tick("recv_grpc", t)
         if self._use_pipeline and self._return_device is None and not M.is_cuda and not E.is_cuda:
             # host result (the reference's recv): staged H2D | decode | D2H into a pinned tensor

@@ -61,6 +61,27 @@ def test_send_recv_roundtrip(comms):
     h.result(timeout=5)
 
 
+def test_readonly_raw_recv_is_a_view(comms):
+    """A hook that only reads the payload (FixedPointHook copying it to the GPU) gets a view of the
+    received message bytes; a plain recv gets its own copy."""
+    from efl.framework import wire
+    leader, follower = comms
+    m = torch.arange(1000, dtype=torch.int64) * 7
+    h = follower.send("m", m)
+    assert torch.equal(leader._recv_raw("m", readonly=True), m)
+    h.result(timeout=5)
+    h = follower.send("m", m)
+    assert torch.equal(leader._recv_raw("m"), m)
+    h.result(timeout=5)
+    payload = m.numpy().tobytes()                         # immutable, like gRPC's request bytes
+    msg = wire.TensorMsg(wire.DT_INT64, (1000,), memoryview(payload), [])
+    base = np.frombuffer(payload, dtype=np.int64).ctypes.data
+    view = efl.Communicator._materialize(msg, None, readonly=True)
+    copy = efl.Communicator._materialize(msg, None)
+    assert view.data_ptr() == base and copy.data_ptr() != base
+    assert torch.equal(view, m) and torch.equal(copy, m)
+
+
 def test_send_completes_only_after_peer_recv(comms):
     leader, follower = comms
     h = follower.send("late", torch.ones(3))
