@@ -320,7 +320,7 @@ class Communicator(object):
         if hasattr(t, "to_hex"):                                  # CipherTensor: DT_STRING on the wire
             t = t.to_hex()
         if isinstance(t, HexTensor):
-            dtype, shape, content = wire.DT_STRING, t.shape, t.to_tensor_content()
+            dtype, shape, content = wire.DT_STRING, t.shape, t.tensor_content_parts()
         else:
             if not isinstance(t, torch.Tensor):
                 t = torch.as_tensor(np.asarray(t))
@@ -387,7 +387,7 @@ class Communicator(object):
         from efl.privacy.hex_tensor import HexTensor
         if msg.dtype == wire.DT_STRING:
             if msg.content is not None and len(msg.content):
-                return HexTensor.from_tensor_content(bytes(msg.content), msg.shape)
+                return HexTensor.from_tensor_content(msg.content, msg.shape)
             return HexTensor.from_strings(np.array(msg.typed, dtype=object).reshape(msg.shape))
         arr = msg.to_numpy()
         if arr.flags.writeable:

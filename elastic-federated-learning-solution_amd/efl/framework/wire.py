@@ -105,13 +105,15 @@ def shape_proto(shape) -> bytes:
 
 
 def tensor_proto_parts(dtype: int, shape, content) -> list:
-    """Parts of a serialized TensorProto (content = bytes-like, not copied)."""
+    """Parts of a serialized TensorProto (content = bytes-like, or a tuple/list of bytes-likes
+    that together form tensor_content; not copied)."""
     sp = shape_proto(shape)
     parts = [key(1, _VARINT) + varint(dtype), _len_field(2, len(sp)) + sp]
-    n = memoryview(content).nbytes
+    pieces = list(content) if isinstance(content, (tuple, list)) else [content]
+    n = sum(memoryview(c).nbytes for c in pieces)
     if n:
         parts.append(_len_field(4, n))
-        parts.append(content)
+        parts.extend(pieces)
     return parts
 
 

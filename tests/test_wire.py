@@ -92,6 +92,28 @@ def test_string_tensor_content_matches_tf_encoding():
     assert back == hx and back.strings() == strs
 
 
+def test_string_length_varints_vectorised():
+    """The numpy varint32 codec of DT_STRING lengths equals the scalar protobuf varint at every
+    width boundary, parses back, and rejects truncated or over-long headers."""
+    from efl.privacy import hex_tensor as ht
+    edges = [0, 1, 127, 128, 16383, 16384, 2**21 - 1, 2**21, 2**28 - 1, 2**28, 2**32 - 1]
+    rng = np.random.default_rng(4)
+    lens = np.array(edges + rng.integers(0, 2**32, 300).tolist() + rng.integers(0, 600, 300).tolist(), np.int64)
+    enc = ht._varint32_encode(lens)
+    assert enc.tobytes() == b"".join(wire.varint(int(v)) for v in lens)
+    tail = np.frombuffer(b"\x05\x80abc", np.uint8)            # bytes after the header do not matter
+    vals, used = ht._varint32_decode(np.concatenate([enc, tail]), lens.size)
+    assert np.array_equal(vals, lens) and used == enc.size
+    with pytest.raises(ValueError):
+        ht._varint32_decode(enc[:-1], lens.size)               # last length cut off
+    with pytest.raises(ValueError):
+        ht._varint32_decode(np.array([0x80] * 6 + [1], np.uint8), 1)
+    with pytest.raises(ValueError):
+        ht._varint32_encode(np.array([2**32]))
+    with pytest.raises(ValueError):                             # lengths promise more bytes than sent
+        efl.HexTensor.from_tensor_content(b"\x05ab", (1,))
+
+
 def test_typed_fields_like_tf_fromproto():
     m = PB["MessageRequest"](name="v", step=1)
     m.tensor.dtype = wire.DT_FLOAT
