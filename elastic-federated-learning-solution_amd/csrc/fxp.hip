@@ -524,11 +524,14 @@ hipError_t launch_tuned(const Shape& sh, const typename Op::Args& a, long long n
   }
 }
 
-// fixed launch (fp64 / integer ops): the fp32 defaults of the same direction
+// fixed launch (fp64 / integer ops): the fp32 default shape of the same direction. Encode: 512
+// lanes, nontemporal loads and `nt sc1` 16-B stores; decode: 128 lanes, nontemporal loads, XCD-aware
+// tile order (round 1 ran both at 128 lanes with nontemporal loads only; tools/bench_fxp_dtypes.py,
+// profiles/r02/fxp_dtypes.jsonl)
 template <class Op>
 hipError_t launch_fixed(int dir, const typename Op::Args& a, long long nunits, hipStream_t s) {
-  (void)dir;
-  return launch_k<Op, 128, 1, 1>(a, nunits, s);
+  if (dir == kEnc) return launch_k<Op, 512, 1, 7>(a, nunits, s);
+  return launch_k<Op, 128, 1, 1>(a, nunits, s, 1);
 }
 
 template <class Op>
