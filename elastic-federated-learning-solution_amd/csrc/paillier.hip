@@ -13,6 +13,8 @@
 // seed with counter = global element index (counter-based: independent of GPU count/launch shape).
 #include "bignum.h"
 #include "common.h"
+
+#include <type_traits>
 #include "pl_common.h"
 
 namespace efl {
@@ -409,16 +411,23 @@ __global__ __launch_bounds__(kPlBlock) void k_powm(Key k, const uint32_t* __rest
 }
 
 // ------------------------------------------------------------------------------------------
-// x^-1 mod n^2 (mpz_invert, paillier.cc:267-285) by binary extended Euclid on an odd modulus:
-// invariants A x = u, C x = v (mod M); u, v, A, C live in the lane's LDS columns (4 x LC words).
-// Trailing zeros are stripped k bits at a time with a Montgomery step (A + ((A*minv) mod 2^k) M is
-// divisible by 2^k). Bounded loop; a non-invertible x yields 0 and reports its index.
+// x^-1 mod n^2 (mpz_invert, paillier.cc:267-285): limb helpers over numbers kept in a lane's LDS
+// column (LdsNum) or, for the Bezout coefficients of keys up to 1024 bits, in registers (RegNum);
+// the kernel (k_invert, Pornin's batched binary GCD) is below.
 // ------------------------------------------------------------------------------------------
 template <int L>
 struct LdsNum {
   uint32_t* p;
   int S;
   __device__ __forceinline__ uint32_t& operator[](int j) const { return p[j * S]; }
+};
+
+// a number in registers: only ever indexed by fully unrolled loops (constant j)
+template <int L>
+struct RegNum {
+  uint32_t v[L];
+  __device__ __forceinline__ uint32_t& operator[](int j) { return v[j]; }
+  __device__ __forceinline__ uint32_t operator[](int j) const { return v[j]; }
 };
 
 template <int L>
@@ -540,11 +549,18 @@ __device__ __forceinline__ void lds_neg(const LdsNum<L>& x, int n) {
 // (u, v) <- the same combinations times 2^-31 mod M (one Montgomery-style step), keeping
 // a = u x, b = v x (mod M). About 2 len(M) / 31 passes of a few limb sweeps each, instead of one
 // sweep per bit; the 31 inner steps are branch-free, so a wave does not diverge in them.
-template <int LN>
+//
+// REG (n^2 of up to 2048 bits): u and v, which every pass sweeps in full, live in registers with
+// the sweeps unrolled; a and b (swept only up to their shrinking top limb) stay in LDS. That halves
+// the LDS per lane and takes four LDS accesses off every limb step of the u, v update: 32,768
+// inverses 1.96 -> 1.66 ms at 1024-bit n, 0.63 -> 0.54 ms at 512-bit; the LDS sweeps of larger keys
+// unrolled by 4, 13.0 -> 12.4 ms at 2048-bit (tools/bench_invert.py, profiles/r02/invert_ab.jsonl).
+template <int LN, bool REG>
 __global__ __launch_bounds__(kPlBlock) void k_invert(Key k, const uint32_t* __restrict__ x,
                                                      uint32_t* __restrict__ out, long long N,
                                                      unsigned long long* bad) {
   constexpr int LC = 2 * LN;
+  constexpr int UR = REG ? LC : 4;    // unroll of the u, v sweeps (full in registers)
   extern __shared__ uint32_t lds[];
   const int S = blockDim.x;
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -552,13 +568,21 @@ __global__ __launch_bounds__(kPlBlock) void k_invert(Key k, const uint32_t* __re
   const uint32_t* M = k.at(k.d.off_n2);
   const uint32_t minv = k.d.n2_minv;   // -M^-1 mod 2^32
   LdsNum<LC> A{lds + threadIdx.x, S}, B{lds + LC * S + threadIdx.x, S};
-  LdsNum<LC> U{lds + 2 * LC * S + threadIdx.x, S}, V{lds + 3 * LC * S + threadIdx.x, S};
+  using UV = typename std::conditional<REG, RegNum<LC>, LdsNum<LC>>::type;
+  UV U, V;
+  if constexpr (!REG) {
+    U = LdsNum<LC>{lds + 2 * LC * S + threadIdx.x, S};
+    V = LdsNum<LC>{lds + 3 * LC * S + threadIdx.x, S};
+  }
   const uint32_t* xi = x + i * LC;
   uint32_t any = 0;
   for (int j = 0; j < LC; ++j) {
     A[j] = xi[j];
     any |= xi[j];
     B[j] = M[j];
+  }
+#pragma unroll UR
+  for (int j = 0; j < LC; ++j) {
     U[j] = j == 0 ? 1u : 0u;
     V[j] = 0u;
   }
@@ -626,6 +650,7 @@ __global__ __launch_bounds__(kPlBlock) void k_invert(Key k, const uint32_t* __re
       const int64_t tu = (int64_t)((s0u * minv) & 0x7FFFFFFFu), tv = (int64_t)((s0v * minv) & 0x7FFFFFFFu);
       int64_t cu = 0, cv = 0;
       uint32_t pu = 0, pv = 0;
+#pragma unroll UR
       for (int j = 0; j < LC; ++j) {
         const int64_t uj = U[j], vj = V[j], mj = M[j];
         const uint32_t ru = signed_limb3(uj * f0, vj * g0, tu * mj, cu);
@@ -642,10 +667,11 @@ __global__ __launch_bounds__(kPlBlock) void k_invert(Key k, const uint32_t* __re
       int64_t eu = cu >> 31, ev = cv >> 31;   // limb LC of the shifted results (small, signed)
 #pragma unroll
       for (int which = 0; which < 2; ++which) {
-        const LdsNum<LC>& R = which ? V : U;
+        UV& R = which ? V : U;
         int64_t& ext = which ? ev : eu;
         while (ext < 0) {   // R += M
           uint32_t c = 0;
+#pragma unroll UR
           for (int j = 0; j < LC; ++j) {
             const uint64_t t = (uint64_t)R[j] + M[j] + c;
             R[j] = (uint32_t)t;
@@ -656,17 +682,30 @@ __global__ __launch_bounds__(kPlBlock) void k_invert(Key k, const uint32_t* __re
         for (;;) {          // R >= M (or ext > 0): R -= M
           bool ge = ext > 0;
           if (!ge) {
-            ge = true;
-            for (int j = LC - 1; j >= 0; --j) {
-              const uint32_t r = R[j], m = M[j];
-              if (r != m) {
-                ge = r > m;
-                break;
+            // R >= M, from the top limb down: branch-free over all limbs in registers (so the
+            // loop stays unrolled), an early exit over LDS (the first differing limb decides)
+            if constexpr (REG) {
+              int cmp = 0;
+#pragma unroll
+              for (int j = LC - 1; j >= 0; --j) {
+                const uint32_t r = R[j], m = M[j];
+                cmp = cmp ? cmp : (r > m) - (r < m);
+              }
+              ge = cmp >= 0;
+            } else {
+              ge = true;
+              for (int j = LC - 1; j >= 0; --j) {
+                const uint32_t r = R[j], m = M[j];
+                if (r != m) {
+                  ge = r > m;
+                  break;
+                }
               }
             }
           }
           if (!ge) break;
           uint32_t br = 0;
+#pragma unroll UR
           for (int j = 0; j < LC; ++j) {
             const uint64_t d = (uint64_t)R[j] - M[j] - br;
             R[j] = (uint32_t)d;
@@ -681,6 +720,7 @@ __global__ __launch_bounds__(kPlBlock) void k_invert(Key k, const uint32_t* __re
   bool ok = a_zero && B[0] == 1u;
   for (int j = 1; j < LC && ok; ++j) ok = B[j] == 0u;
   uint32_t* o = out + i * LC;
+#pragma unroll UR
   for (int j = 0; j < LC; ++j) o[j] = ok ? V[j] : 0u;
   if (!ok) atomicMin(bad, (unsigned long long)i);
 }
@@ -966,9 +1006,10 @@ template <int LN>
 hipError_t run_invert(Key k, const uint32_t* x, uint32_t* out, long long N, unsigned long long* bad, hipStream_t s) {
   // four LDS numbers per lane: 32 lanes per workgroup for n^2 of 8192 bits (128 KiB)
   constexpr int block = LN >= 128 ? 32 : kPlBlock;
-  const size_t lds = (size_t)4 * (2 * LN) * block * 4;
-  hipLaunchKernelGGL((k_invert<LN>), dim3((unsigned)((N + block - 1) / block)), dim3(block), lds, s, k, x, out, N,
-                     bad);
+  constexpr bool reg = 2 * LN <= 64;   // u, v in registers (k_invert)
+  const size_t lds = (size_t)(reg ? 2 : 4) * (2 * LN) * block * 4;
+  hipLaunchKernelGGL((k_invert<LN, reg>), dim3((unsigned)((N + block - 1) / block)), dim3(block), lds, s, k, x, out,
+                     N, bad);
   return hipGetLastError();
 }
 template <int LN>
