@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import threading
 import types
 
 import numpy as np
@@ -164,15 +165,40 @@ def back(t: torch.Tensor, home: torch.device) -> torch.Tensor:
     return t.to(home)
 
 
+# Host tensors from this many elements on take the pinned three-stream pipeline
+# (efl.framework.host_pipeline: chunked H2D | codec | D2H, outputs in pinned memory) instead of one
+# pageable H2D, the kernel and one pageable D2H back to back: the reference's ops are CPU ops, so a
+# drop-in caller hands over host tensors.
+HOST_PIPELINE_MIN_ELEMS = 1 << 22
+_pipes: dict = {}
+_pipes_lock = threading.Lock()
+
+
+def _host_pipeline():
+    """(pipeline, lock) of the current GPU; one caller at a time uses a pipeline's slots."""
+    dev = require_gpu()
+    with _pipes_lock:
+        entry = _pipes.get(dev)
+        if entry is None:
+            from efl.framework.host_pipeline import PinnedCodecPipeline   # imports this module
+            entry = _pipes[dev] = (PinnedCodecPipeline(dev), threading.Lock())
+    return entry
+
+
 # ----------------------------------------------------------------------------------------------
 # ops (fed_ops names)
 # ----------------------------------------------------------------------------------------------
 
 def convert_to_fixed_point(t, decrease_precision=None):
     """REGISTER_OP("ConvertToFixedPoint") (efls-train/cc/efl/math/fixed_point.cc:24-40).
-    Returns (mantissa int64, exponent int64) of t's shape, on t's device."""
+    Returns (mantissa int64, exponent int64) of t's shape, on t's device (pinned host memory for
+    large host tensors, which go through the pipelined copies)."""
     t = as_tensor(t)
     code = dt_code(t.dtype)
+    if not t.is_cuda and t.numel() >= HOST_PIPELINE_MIN_ELEMS:
+        pipe, lock = _host_pipeline()
+        with lock:
+            return pipe.encode(t, decrease_precision=bool(decrease_precision))
     x, home = on_device(t)
     M = torch.empty(x.shape, dtype=torch.int64, device=x.device)
     E = torch.empty(x.shape, dtype=torch.int64, device=x.device)
@@ -207,6 +233,12 @@ def fixed_point_to_float_point(mantissa, exponent, dtype=torch.float32, flush_de
     mantissa = as_tensor(mantissa)
     if mantissa.dtype != torch.int64 or exponent.dtype != torch.int64:
         raise errors.InvalidArgumentError("FixedPointToFloatPoint: mantissa and exponent must be int64")
+    if not mantissa.is_cuda and not exponent.is_cuda and mantissa.numel() >= HOST_PIPELINE_MIN_ELEMS:
+        if mantissa.numel() != exponent.numel():
+            raise errors.InvalidArgumentError("mantissa and exponent should be the same size.")
+        pipe, lock = _host_pipeline()
+        with lock:
+            return pipe.decode(mantissa, exponent, dtype, flush_denormal=ftz)
     m, home = on_device(mantissa)
     e, _ = on_device(exponent)
     if e.device != m.device:

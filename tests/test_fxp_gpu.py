@@ -240,6 +240,31 @@ def test_shapes_and_host_staging(efl):
     assert y.device.type == "cpu" and torch.equal(y, x)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64, torch.int32])
+def test_large_host_tensors_take_the_pipeline(efl, dtype):
+    """Host tensors of HOST_PIPELINE_MIN_ELEMS or more go through the pinned three-stream pipeline
+    (several chunks and a ragged last one here, a pageable source, a non-contiguous view): the same
+    bits as the device path, back on the host, for both directions and decrease_precision."""
+    n = efl.lib.HOST_PIPELINE_MIN_ELEMS * 2 + 77
+    g = torch.Generator().manual_seed(9)
+    if dtype.is_floating_point:
+        base = torch.randn(n + 1, generator=g, dtype=dtype)
+        base[:4] = torch.tensor([0.0, -0.0, 2.0 ** 23 + 1, 1e-40], dtype=dtype)
+    else:
+        base = torch.randint(-2**31, 2**31 - 1, (n + 1,), generator=g, dtype=dtype)
+    x = base[1:]                                     # offset view of a pageable tensor
+    for dp in (False, True):
+        M, E = efl.lib.ops.convert_to_fixed_point(x, decrease_precision=dp)
+        Md, Ed = efl.lib.ops.convert_to_fixed_point(x.cuda(), decrease_precision=dp)
+        assert M.device.type == "cpu" and M.shape == x.shape
+        assert torch.equal(M, Md.cpu()) and torch.equal(E, Ed.cpu())
+    if dtype.is_floating_point:
+        y = efl.lib.ops.fixed_point_to_float_point(M, E, dtype)
+        yd = efl.lib.ops.fixed_point_to_float_point(Md, Ed, dtype)
+        assert y.device.type == "cpu" and y.dtype == dtype
+        assert torch.equal(y.view(-1).view(torch.uint8), yd.cpu().view(-1).view(torch.uint8))
+
+
 def test_errors(efl):
     with pytest.raises(efl.errors.InvalidArgumentError, match="same size"):
         efl.lib.ops.fixed_point_to_float_point(dev(np.zeros(4, np.int64)), dev(np.zeros(5, np.int64)))
