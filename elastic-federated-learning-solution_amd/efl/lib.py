@@ -168,7 +168,8 @@ def back(t: torch.Tensor, home: torch.device) -> torch.Tensor:
 # Host tensors from this many elements on take the pinned three-stream pipeline
 # (efl.framework.host_pipeline: chunked H2D | codec | D2H, outputs in pinned memory) instead of one
 # pageable H2D, the kernel and one pageable D2H back to back: the reference's ops are CPU ops, so a
-# drop-in caller hands over host tensors.
+# drop-in caller hands over host tensors. The pipeline of a GPU keeps its device
+# chunk slots (about 250 MiB for fp32 encode + decode) and pinned staging chunks after first use.
 HOST_PIPELINE_MIN_ELEMS = 1 << 22
 _pipes: dict = {}
 _pipes_lock = threading.Lock()
