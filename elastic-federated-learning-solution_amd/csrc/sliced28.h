@@ -24,6 +24,11 @@
 namespace efl {
 namespace s28 {
 
+// unroll of the CIOS step loop (build knob; 1 = one step per loop pass)
+#ifndef EFL_MONT28_UNROLL
+#define EFL_MONT28_UNROLL 1
+#endif
+
 constexpr int kBits = 28;
 constexpr uint32_t kMask = (1u << kBits) - 1;
 
@@ -93,7 +98,7 @@ __device__ __forceinline__ void mont_mul(uint32_t (&a)[C], const B& b, const uin
   uint64_t T[C];
 #pragma unroll
   for (int j = 0; j < C; ++j) T[j] = 0;
-#pragma unroll 1
+#pragma unroll EFL_MONT28_UNROLL
   for (int i = 0; i < L; ++i) {
     const uint32_t bi = b(i);
 #pragma unroll
