@@ -24,9 +24,13 @@
 namespace efl {
 namespace s28 {
 
-// unroll of the CIOS step loop (build knob; 1 = one step per loop pass)
+// Unroll of the CIOS step loop for numbers sliced over G >= 2 lanes (build knob). Two steps per
+// loop pass: same-box A/B (profiles/r02/ab_mont_unroll.jsonl) 1024-bit encrypt +2-4 %, 4096-bit
+// encrypt +5 %, 4096-bit decrypt +2 %, MNIST matmul +1 %. G = 1 (the 1024-bit decryption's
+// one-lane family) keeps one step per pass: unrolled, its register spills grew 191 -> 1087 VGPRs
+// and it ran 7.6x slower.
 #ifndef EFL_MONT28_UNROLL
-#define EFL_MONT28_UNROLL 1
+#define EFL_MONT28_UNROLL 2
 #endif
 
 constexpr int kBits = 28;
@@ -95,10 +99,11 @@ template <int C, int G, class B>
 __device__ __forceinline__ void mont_mul(uint32_t (&a)[C], const B& b, const uint32_t (&m)[C], uint32_t minv,
                                          int g) {
   constexpr int L = C * G;
+  constexpr int kUnroll = G == 1 ? 1 : EFL_MONT28_UNROLL;
   uint64_t T[C];
 #pragma unroll
   for (int j = 0; j < C; ++j) T[j] = 0;
-#pragma unroll EFL_MONT28_UNROLL
+#pragma unroll kUnroll
   for (int i = 0; i < L; ++i) {
     const uint32_t bi = b(i);
 #pragma unroll
