@@ -371,13 +371,14 @@ __global__ __launch_bounds__(kPlBlock) void k_add(Key k, const uint32_t* __restr
   store_g<LC>(out + i * LC, a);
 }
 
-// c = x^e mod n^2 for a per-element non-negative exponent of `ewords` 32-bit words
-// (MulScalar / MulExp2, paillier.cc:180-265, 683-719; a negative scalar arrives with x already
-// inverted). exps: [N][ewords].
-template <int LN>
-__global__ __launch_bounds__(kPlBlock) void k_powm(Key k, const uint32_t* __restrict__ x,
-                                                   const uint32_t* __restrict__ exps, int ewords,
-                                                   uint32_t* __restrict__ out, long long N) {
+// c = x^e mod n^2 for a per-element non-negative exponent read through `xs` (pl_common.h: 32-bit
+// words, |int64| or 2^int64; MulScalar / MulExp2, paillier.cc:180-265, 683-719; a negative scalar
+// is finished by an inversion, efl_pl_mul_scalar). Elements whose exponent is not ok get 0 and
+// their index in `bad`.
+template <int LN, class XS>
+__global__ __launch_bounds__(kPlBlock) void k_powm(Key k, const uint32_t* __restrict__ x, XS xs,
+                                                   uint32_t* __restrict__ out, long long N,
+                                                   unsigned long long* bad) {
   constexpr int LC = 2 * LN;
   extern __shared__ uint32_t lds[];
   const int S = blockDim.x;
@@ -386,16 +387,15 @@ __global__ __launch_bounds__(kPlBlock) void k_powm(Key k, const uint32_t* __rest
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N) return;
   const uint32_t* n2 = k.at(k.d.off_n2);
-  const uint32_t* e = exps + i * ewords;
-  int ebits = 0;
-  for (int w = ewords - 1; w >= 0; --w)
-    if (e[w]) { ebits = w * 32 + 32 - __clz(e[w]); break; }
+  const auto ex = xs.at(i);
+  const int ebits = ex.ok ? ex.bits() : 0;
   uint32_t t[LC];
   if (ebits == 0) {
     // x^0 = 1 (mpz_powm: 1 mod n^2)
 #pragma unroll
-    for (int j = 0; j < LC; ++j) t[j] = j == 0 ? 1u : 0u;
+    for (int j = 0; j < LC; ++j) t[j] = (ex.ok && j == 0) ? 1u : 0u;
     store_g<LC>(out + i * LC, t);
+    if (!ex.ok) atomicMin(bad, (unsigned long long)i);
     return;
   }
   load_g<LC>(t, x + i * LC);
@@ -404,7 +404,7 @@ __global__ __launch_bounds__(kPlBlock) void k_powm(Key k, const uint32_t* __rest
 #pragma unroll 1
   for (int b = ebits - 2; b >= 0; --b) {
     mont_sqr<LC>(t, acol, S, n2, k.d.n2_minv);
-    if ((e[b >> 5] >> (b & 31)) & 1u) mont_mul<LC>(t, LdsCol{bcol, S}, n2, k.d.n2_minv);
+    if (ex.bit(b)) mont_mul<LC>(t, LdsCol{bcol, S}, n2, k.d.n2_minv);
   }
   redc<LC>(t, n2, k.d.n2_minv);
   store_g<LC>(out + i * LC, t);
@@ -555,16 +555,28 @@ __device__ __forceinline__ void lds_neg(const LdsNum<L>& x, int n) {
 // the LDS per lane and takes four LDS accesses off every limb step of the u, v update: 32,768
 // inverses 1.96 -> 1.66 ms at 1024-bit n, 0.63 -> 0.54 ms at 512-bit; the LDS sweeps of larger keys
 // unrolled by 4, 13.0 -> 12.4 ms at 2048-bit (tools/bench_invert.py, profiles/r02/invert_ab.jsonl).
+//
+// sel_kind selects the elements to invert (the others are copied, or left alone when out == x; x
+// is read in full before out is written, so the op runs in place): 0 every element, 1 where the
+// int8 flag sel[i] != 0 (a parsed hex scalar's sign), 2 where the int64 sel[i] < 0 (MulScalar's y).
 template <int LN, bool REG>
-__global__ __launch_bounds__(kPlBlock) void k_invert(Key k, const uint32_t* __restrict__ x,
-                                                     uint32_t* __restrict__ out, long long N,
-                                                     unsigned long long* bad) {
+__global__ __launch_bounds__(kPlBlock) void k_invert(Key k, const uint32_t* x, uint32_t* out, long long N,
+                                                     unsigned long long* bad, const void* sel, int sel_kind) {
   constexpr int LC = 2 * LN;
   constexpr int UR = REG ? LC : 4;    // unroll of the u, v sweeps (full in registers)
   extern __shared__ uint32_t lds[];
   const int S = blockDim.x;
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N) return;
+  if (sel_kind) {
+    const bool inv = sel_kind == 1 ? ((const signed char*)sel)[i] != 0 : ((const long long*)sel)[i] < 0;
+    if (!inv) {
+      if (out != x)
+        for (int j = 0; j < LC; j += 4)
+          *reinterpret_cast<uint4*>(out + i * LC + j) = *reinterpret_cast<const uint4*>(x + i * LC + j);
+      return;
+    }
+  }
   const uint32_t* M = k.at(k.d.off_n2);
   const uint32_t minv = k.d.n2_minv;   // -M^-1 mod 2^32
   LdsNum<LC> A{lds + threadIdx.x, S}, B{lds + LC * S + threadIdx.x, S};
@@ -994,24 +1006,41 @@ struct RunAdd {
 };
 template <int LN>
 struct RunPowm {
-  static hipError_t run(Key k, const uint32_t* x, const uint32_t* e, int ew, uint32_t* out, long long N,
+  template <class XS>
+  static hipError_t run(Key k, const uint32_t* x, XS xs, uint32_t* out, long long N, unsigned long long* bad,
                         hipStream_t s) {
     const size_t lds = (size_t)2 * (2 * LN) * kPlBlock * 4;
-    hipLaunchKernelGGL((k_powm<LN>), dim3(grid_of(N)), dim3(kPlBlock), lds, s, k, x, e, ew, out, N);
+    hipLaunchKernelGGL((k_powm<LN, XS>), dim3(grid_of(N)), dim3(kPlBlock), lds, s, k, x, xs, out, N, bad);
     return hipGetLastError();
   }
 };
 
 template <int LN>
-hipError_t run_invert(Key k, const uint32_t* x, uint32_t* out, long long N, unsigned long long* bad, hipStream_t s) {
+hipError_t run_invert(Key k, const uint32_t* x, uint32_t* out, long long N, unsigned long long* bad, hipStream_t s,
+                      const void* sel = nullptr, int sel_kind = 0) {
   // four LDS numbers per lane: 32 lanes per workgroup for n^2 of 8192 bits (128 KiB)
   constexpr int block = LN >= 128 ? 32 : kPlBlock;
   constexpr bool reg = 2 * LN <= 64;   // u, v in registers (k_invert)
   const size_t lds = (size_t)(reg ? 2 : 4) * (2 * LN) * block * 4;
   hipLaunchKernelGGL((k_invert<LN, reg>), dim3((unsigned)((N + block - 1) / block)), dim3(block), lds, s, k, x, out,
-                     N, bad);
+                     N, bad, sel, sel_kind);
   return hipGetLastError();
 }
+
+hipError_t invert_ln(Key k, const uint32_t* x, uint32_t* out, long long N, unsigned long long* bad, hipStream_t s,
+                     const void* sel, int sel_kind) {
+  switch (k.d.ln) {
+    case 16: return run_invert<16>(k, x, out, N, bad, s, sel, sel_kind);
+    case 32: return run_invert<32>(k, x, out, N, bad, s, sel, sel_kind);
+    case 64: return run_invert<64>(k, x, out, N, bad, s, sel, sel_kind);
+    default: return run_invert<128>(k, x, out, N, bad, s, sel, sel_kind);
+  }
+}
+
+// z = x^e mod n^2 with the exponent source xs, in the family chosen for n^2 ops
+template <class XS>
+hipError_t powm_family(Key k, const uint32_t* x, XS xs, uint32_t* z, long long n, unsigned long long* bad,
+                       hipStream_t s);
 template <int LN>
 struct RunMatmul {
   static hipError_t run(Key k, const uint32_t* X, const long long* xe, const long long* ym, const long long* ye,
@@ -1106,8 +1135,112 @@ EFL_API int efl_pl_powm(const void* key_block, const efl_pl_key* key, const uint
   Key k{(const uint32_t*)key_block, *key};
   const int C = slicing(key->ln, 0);
   return hip_status(C ? pl::sl_powm(k, C, x, exps, exp_words, z, (long long)n, (hipStream_t)stream)
-                      : dispatch_ln<RunPowm>(key->ln, k, x, exps, exp_words, z, (long long)n, (hipStream_t)stream),
+                      : dispatch_ln<RunPowm>(key->ln, k, x, pl::ExpWords{exps, exp_words}, z, (long long)n,
+                                             (unsigned long long*)nullptr, (hipStream_t)stream),
                     "efl_pl_powm");
+}
+
+namespace efl {
+namespace {
+template <>
+hipError_t powm_family<pl::ExpAbs64>(Key k, const uint32_t* x, pl::ExpAbs64 xs, uint32_t* z, long long n,
+                                     unsigned long long* bad, hipStream_t s) {
+  const int C = slicing(k.d.ln, 0);
+  return C ? pl::sl_powm_abs64(k, C, x, xs.y, z, n, bad, s) : dispatch_ln<RunPowm>(k.d.ln, k, x, xs, z, n, bad, s);
+}
+template <>
+hipError_t powm_family<pl::ExpPow2>(Key k, const uint32_t* x, pl::ExpPow2 xs, uint32_t* z, long long n,
+                                    unsigned long long* bad, hipStream_t s) {
+  const int C = slicing(k.d.ln, 0);
+  return C ? pl::sl_powm_pow2(k, C, x, xs.y, z, n, bad, s) : dispatch_ln<RunPowm>(k.d.ln, k, x, xs, z, n, bad, s);
+}
+template <>
+hipError_t powm_family<pl::ExpShift>(Key k, const uint32_t* x, pl::ExpShift xs, uint32_t* z, long long n,
+                                     unsigned long long* bad, hipStream_t s) {
+  const int C = slicing(k.d.ln, 0);
+  return C ? pl::sl_powm_shift(k, C, x, xs.own, xs.other, z, n, bad, s)
+           : dispatch_ln<RunPowm>(k.d.ln, k, x, xs, z, n, bad, s);
+}
+template <>
+hipError_t powm_family<pl::ExpWords>(Key k, const uint32_t* x, pl::ExpWords xs, uint32_t* z, long long n,
+                                     unsigned long long* bad, hipStream_t s) {
+  const int C = slicing(k.d.ln, 0);
+  return C ? pl::sl_powm(k, C, x, xs.e, xs.ew, z, n, s) : dispatch_ln<RunPowm>(k.d.ln, k, x, xs, z, n, bad, s);
+}
+
+// common prologue of the ops with a device status word: argument checks, bad <- -1
+int status_prologue(const efl_pl_key* key, int64_t n, int64_t* bad, hipStream_t s, const char* op) {
+  if (!key_ok(key, false, 128)) return EFL_E_INVALID_ARGUMENT;
+  if (!bad) { set_error("%s: null status word", op); return EFL_E_INVALID_ARGUMENT; }
+  if (n < 0) { set_error("%s: negative count", op); return EFL_E_INVALID_ARGUMENT; }
+  return hip_status(hipMemsetAsync(bad, 0xFF, sizeof(int64_t), s), op);
+}
+}  // namespace
+}  // namespace efl
+
+EFL_API int efl_pl_mul_exp2(const void* key_block, const efl_pl_key* key, const uint32_t* x, const int64_t* y,
+                            uint32_t* z, int64_t n, int64_t* bad, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int rc = status_prologue(key, n, bad, s, "efl_pl_mul_exp2");
+  if (rc != EFL_OK || n == 0) return rc;
+  Key k{(const uint32_t*)key_block, *key};
+  return hip_status(powm_family(k, x, pl::ExpPow2{(const long long*)y}, z, (long long)n, (unsigned long long*)bad, s),
+                    "efl_pl_mul_exp2");
+}
+
+EFL_API int efl_pl_mul_scalar(const void* key_block, const efl_pl_key* key, const uint32_t* x, const int64_t* y,
+                              uint32_t* z, int64_t n, int64_t* bad, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int rc = status_prologue(key, n, bad, s, "efl_pl_mul_scalar");
+  if (rc != EFL_OK || n == 0) return rc;
+  Key k{(const uint32_t*)key_block, *key};
+  unsigned long long* b = (unsigned long long*)bad;
+  hipError_t e = powm_family(k, x, pl::ExpAbs64{(const long long*)y}, z, (long long)n, b, s);
+  if (e == hipSuccess) e = invert_ln(k, z, z, (long long)n, b, s, y, 2);
+  return hip_status(e, "efl_pl_mul_scalar");
+}
+
+EFL_API int efl_pl_mul_scalar_big(const void* key_block, const efl_pl_key* key, const uint32_t* x,
+                                  const uint32_t* y_magnitude, int y_words, const int8_t* y_negative, uint32_t* z,
+                                  int64_t n, int64_t* bad, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int rc = status_prologue(key, n, bad, s, "efl_pl_mul_scalar_big");
+  if (rc != EFL_OK || n == 0) return rc;
+  if (y_words <= 0) { set_error("y_words must be positive"); return EFL_E_INVALID_ARGUMENT; }
+  Key k{(const uint32_t*)key_block, *key};
+  unsigned long long* b = (unsigned long long*)bad;
+  hipError_t e = powm_family(k, x, pl::ExpWords{y_magnitude, y_words}, z, (long long)n, b, s);
+  if (e == hipSuccess && y_negative) e = invert_ln(k, z, z, (long long)n, b, s, y_negative, 1);
+  return hip_status(e, "efl_pl_mul_scalar_big");
+}
+
+EFL_API int efl_pl_fxp_add(const void* key_block, const efl_pl_key* key, const uint32_t* x, const int64_t* x_exponent,
+                           const uint32_t* y, const int64_t* y_exponent, uint32_t* z, int64_t n, int64_t* bad,
+                           void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int rc = status_prologue(key, n, bad, s, "efl_pl_fxp_add");
+  if (rc != EFL_OK || n == 0) return rc;
+  Key k{(const uint32_t*)key_block, *key};
+  unsigned long long* b = (unsigned long long*)bad;
+  const long long* xe = (const long long*)x_exponent;
+  const long long* ye = (const long long*)y_exponent;
+  const int C = slicing(key->ln, 0);
+  if (C) {
+    const hipError_t e = pl::sl_fxp_add(k, C, x, xe, y, ye, z, (long long)n, b, s);
+    if (e != hipErrorNotSupported) return hip_status(e, "efl_pl_fxp_add");
+  }
+  // families without the fused kernel: the reference's composition, (x << dl) + (y << dr)
+  uint32_t* tmp = nullptr;
+  const size_t words = (size_t)n * 2 * key->ln;
+  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&tmp), 2 * words * 4, s);
+  if (e != hipSuccess) return hip_status(e, "efl_pl_fxp_add");
+  e = powm_family(k, x, pl::ExpShift{xe, ye}, tmp, (long long)n, b, s);
+  if (e == hipSuccess) e = powm_family(k, y, pl::ExpShift{ye, xe}, tmp + words, (long long)n, b, s);
+  if (e == hipSuccess)
+    e = C ? pl::sl_add(k, C, tmp, tmp + words, z, (long long)n, s)
+          : dispatch_ln<RunAdd>(key->ln, k, tmp, tmp + words, z, (long long)n, s);
+  const hipError_t fe = hipFreeAsync(tmp, s);
+  return hip_status(e != hipSuccess ? e : fe, "efl_pl_fxp_add");
 }
 
 EFL_API int efl_pl_invert(const void* key_block, const efl_pl_key* key, const uint32_t* x, uint32_t* z,

@@ -308,25 +308,25 @@ __global__ __launch_bounds__(kSlBlock) SL_OCC void k_add(Key k, const uint32_t* 
   store_slice<C>(out + i * L, g, a);
 }
 
-template <int C, int G>
-__global__ __launch_bounds__(kSlBlock) SL_OCC void k_powm(Key k, const uint32_t* __restrict__ x,
-                                                   const uint32_t* __restrict__ exps, int ewords,
-                                                   uint32_t* __restrict__ out, long long N) {
+// x^e mod n^2 with the per-element exponent of `xs` (pl_common.h: words, |int64| or 2^int64)
+template <int C, int G, class XS>
+__global__ __launch_bounds__(kSlBlock) SL_OCC void k_powm(Key k, const uint32_t* __restrict__ x, XS xs,
+                                                   uint32_t* __restrict__ out, long long N,
+                                                   unsigned long long* bad) {
   constexpr int L = C * G, E = kSlBlock / G;
   extern __shared__ uint32_t lds[];
   SL_ELEMENT(E, G)
   if (i >= N) return;
   uint32_t* BASE = lds + e;
   uint32_t* SCR = lds + L * E + e;
-  const uint32_t* ex = exps + i * ewords;
-  int ebits = 0;
-  for (int w = ewords - 1; w >= 0; --w)
-    if (ex[w]) { ebits = w * 32 + 32 - __clz(ex[w]); break; }
+  const auto ex = xs.at(i);
+  const int ebits = ex.ok ? ex.bits() : 0;
   uint32_t t[C];
   if (ebits == 0) {
 #pragma unroll
-    for (int j = 0; j < C; ++j) t[j] = (g == 0 && j == 0) ? 1u : 0u;
+    for (int j = 0; j < C; ++j) t[j] = (ex.ok && g == 0 && j == 0) ? 1u : 0u;
     store_slice<C>(out + i * L, g, t);
+    if (!ex.ok && g == 0) atomicMin(bad, (unsigned long long)i);
     return;
   }
   uint32_t n2[C];
@@ -338,7 +338,7 @@ __global__ __launch_bounds__(kSlBlock) SL_OCC void k_powm(Key k, const uint32_t*
 #pragma unroll 1
   for (int b = ebits - 2; b >= 0; --b) {
     mont_sqr<C, G>(t, SCR, E, n2, minv, g);
-    if ((ex[b >> 5] >> (b & 31)) & 1u) mont_mul<C, G>(t, LdsElem{BASE, E}, n2, minv, g);
+    if (ex.bit(b)) mont_mul<C, G>(t, LdsElem{BASE, E}, n2, minv, g);
   }
   redc<C, G>(t, n2, minv, g);
   store_slice<C>(out + i * L, g, t);
@@ -362,11 +362,14 @@ __device__ __forceinline__ void to_mont28(uint32_t (&t)[s28::limbs_per_lane(C * 
   s28::mont_mul<C28, G>(t, Uniform{k.at(k.d.off_n2_r2_28)}, m28, k.d.n2_minv28, g);
 }
 
-// normal form (< n^2) from a radix-2^28 Montgomery slice, stored as 32-bit words
+// normal form (< n^2) from a radix-2^28 Montgomery slice, stored as 32-bit words. The final
+// reduction leaves a residue of 0 as either 0 or m (lazy bound <= m); with `m32` (the modulus in
+// 32-bit words) an m is written as 0, as mpz_powm gives for a non-unit x (e.g. n^2 mod n^2).
 template <int C, int G>
 __device__ __forceinline__ void store_from_mont28(uint32_t* out, uint32_t (&t)[s28::limbs_per_lane(C * G, G)],
                                                   const uint32_t (&m28)[s28::limbs_per_lane(C * G, G)],
-                                                  uint32_t minv28, uint32_t* SCR, int E, int g) {
+                                                  uint32_t minv28, uint32_t* SCR, int E, int g,
+                                                  const uint32_t* m32 = nullptr) {
   constexpr int L = C * G, C28 = s28::limbs_per_lane(L, G), L28 = C28 * G;
   s28::mont_mul<C28, G>(t, Unit{}, m28, minv28, g);
   lds_sync();
@@ -374,6 +377,14 @@ __device__ __forceinline__ void store_from_mont28(uint32_t* out, uint32_t (&t)[s
   lds_sync();
   uint32_t w[C];
   s28::to_words<C>(w, SCR, E, L28, g);
+  if (m32) {
+    uint32_t m[C];
+    slice_uniform<C>(m, m32, g);
+    if (geq<C, G>(w, m, g)) {
+#pragma unroll
+      for (int j = 0; j < C; ++j) w[j] = 0u;
+    }
+  }
   store_slice<C>(out, g, w);
 }
 
@@ -420,10 +431,10 @@ __global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_encry
   store_from_mont28<C, G>(out + i * L, acc, m28, k.d.n2_minv28, B, E, g);
 }
 
-template <int C, int G>
+template <int C, int G, class XS>
 __global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_powm28(Key k, const uint32_t* __restrict__ x,
-                                                                       const uint32_t* __restrict__ exps, int ewords,
-                                                                       uint32_t* __restrict__ out, long long N) {
+                                                                       XS xs, uint32_t* __restrict__ out,
+                                                                       long long N, unsigned long long* bad) {
   constexpr int L = C * G, E = kSlBlock / G;
   constexpr int C28 = s28::limbs_per_lane(L, G), L28 = C28 * G;
   extern __shared__ uint32_t lds[];
@@ -431,15 +442,14 @@ __global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_powm2
   if (i >= N) return;
   uint32_t* BASE = lds + e;
   uint32_t* SCR = lds + L28 * E + e;
-  const uint32_t* ex = exps + i * ewords;
-  int ebits = 0;
-  for (int w = ewords - 1; w >= 0; --w)
-    if (ex[w]) { ebits = w * 32 + 32 - __clz(ex[w]); break; }
+  const auto ex = xs.at(i);
+  const int ebits = ex.ok ? ex.bits() : 0;
   if (ebits == 0) {
     uint32_t one[C];
 #pragma unroll
-    for (int j = 0; j < C; ++j) one[j] = (g == 0 && j == 0) ? 1u : 0u;
+    for (int j = 0; j < C; ++j) one[j] = (ex.ok && g == 0 && j == 0) ? 1u : 0u;
     store_slice<C>(out + i * L, g, one);
+    if (!ex.ok && g == 0) atomicMin(bad, (unsigned long long)i);
     return;
   }
   uint32_t m28[C28], t[C28];
@@ -451,9 +461,53 @@ __global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_powm2
 #pragma unroll 1
   for (int b = ebits - 2; b >= 0; --b) {
     s28::mont_sqr<C28, G>(t, SCR, E, m28, minv28, g);
-    if ((ex[b >> 5] >> (b & 31)) & 1u) s28::mont_mul<C28, G>(t, LdsElem{BASE, E}, m28, minv28, g);
+    if (ex.bit(b)) s28::mont_mul<C28, G>(t, LdsElem{BASE, E}, m28, minv28, g);
   }
-  store_from_mont28<C, G>(out + i * L, t, m28, minv28, SCR, E, g);
+  store_from_mont28<C, G>(out + i * L, t, m28, minv28, SCR, E, g, k.at(k.d.off_n2));
+}
+
+// FixedPointTensor.__add__ (paillier.py:116-133) in one launch: z = x^(2^(xe - m)) y^(2^(ye - m))
+// mod n^2, m = min(xe, ye). The reference shifts both sides with PaillierMulExp2 (one of the two
+// shifts is 2^0) and multiplies them with PaillierAdd: three ops, each a pass over HBM. Here the
+// side with the larger exponent is squared d = |xe - ye| times and multiplied by the other side
+// once: d + 4 radix-2^28 products (two conversions in, one out) instead of d + 6 over three launches.
+// d > kMaxShift -> z = 0 and the index into bad (the caller raises, like a MulExp2 shift past it).
+template <int C, int G>
+__global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_fxp_add28(
+    Key k, const uint32_t* __restrict__ x, const long long* __restrict__ xe, const uint32_t* __restrict__ y,
+    const long long* __restrict__ ye, uint32_t* __restrict__ out, long long N, unsigned long long* bad) {
+  constexpr int L = C * G, E = kSlBlock / G;
+  constexpr int C28 = s28::limbs_per_lane(L, G), L28 = C28 * G;
+  extern __shared__ uint32_t lds[];
+  SL_ELEMENT(E, G)
+  if (i >= N) return;
+  uint32_t* BASE = lds + e;
+  uint32_t* SCR = lds + L28 * E + e;
+  const long long a = xe[i], b = ye[i];
+  const bool shift_x = a > b;
+  const uint64_t d = shift_x ? (uint64_t)a - (uint64_t)b : (uint64_t)b - (uint64_t)a;
+  if (d > (uint64_t)kMaxShift) {
+    uint32_t zero[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) zero[j] = 0u;
+    store_slice<C>(out + i * L, g, zero);
+    if (g == 0) atomicMin(bad, (unsigned long long)i);
+    return;
+  }
+  const uint32_t* A = (shift_x ? x : y) + i * L;   // raised to 2^d
+  const uint32_t* B = (shift_x ? y : x) + i * L;
+  uint32_t m28[C28], t[C28];
+  slice_uniform<C28>(m28, k.at(k.d.off_n2_28), g);
+  const uint32_t minv28 = k.d.n2_minv28;
+  to_mont28<C, G>(t, B, k, m28, SCR, E, g);        // B R
+  lds_sync();
+  to_lds<C28>(BASE, E, g, t);
+  to_mont28<C, G>(t, A, k, m28, SCR, E, g);        // A R
+#pragma unroll 1
+  for (int s = 0; s < (int)d; ++s) s28::mont_sqr<C28, G>(t, SCR, E, m28, minv28, g);
+  lds_sync();
+  s28::mont_mul<C28, G>(t, LdsElem{BASE, E}, m28, minv28, g);   // A^(2^d) B R
+  store_from_mont28<C, G>(out + i * L, t, m28, minv28, SCR, E, g, k.at(k.d.off_n2));
 }
 
 // ---- PaillierMatmul in radix 2^28: x converted once, then one multi-exponentiation per output ----
@@ -1221,11 +1275,18 @@ hipError_t run_fbpowm28(const Key& k, const uint32_t* a, uint32_t* out, long lon
   hipLaunchKernelGGL((k_fbpowm28<C, G>), dim3(grid_of(N, G)), dim3(kSlBlock), lds, s, k, a, out, N, seed, ctr0);
   return hipGetLastError();
 }
-template <int C, int G>
-hipError_t run_powm28(const Key& k, const uint32_t* x, const uint32_t* e, int ew, uint32_t* out, long long N,
+template <int C, int G, class XS>
+hipError_t run_powm28(const Key& k, const uint32_t* x, XS xs, uint32_t* out, long long N, unsigned long long* bad,
                       hipStream_t s) {
   const size_t lds = (size_t)(2 * s28::limbs_per_lane(C * G, G) * G) * (kSlBlock / G) * 4;
-  hipLaunchKernelGGL((k_powm28<C, G>), dim3(grid_of(N, G)), dim3(kSlBlock), lds, s, k, x, e, ew, out, N);
+  hipLaunchKernelGGL((k_powm28<C, G, XS>), dim3(grid_of(N, G)), dim3(kSlBlock), lds, s, k, x, xs, out, N, bad);
+  return hipGetLastError();
+}
+template <int C, int G>
+hipError_t run_fxp_add28(const Key& k, const uint32_t* x, const long long* xe, const uint32_t* y, const long long* ye,
+                         uint32_t* out, long long N, unsigned long long* bad, hipStream_t s) {
+  const size_t lds = (size_t)(2 * s28::limbs_per_lane(C * G, G) * G) * (kSlBlock / G) * 4;
+  hipLaunchKernelGGL((k_fxp_add28<C, G>), dim3(grid_of(N, G)), dim3(kSlBlock), lds, s, k, x, xe, y, ye, out, N, bad);
   return hipGetLastError();
 }
 template <int C, int G>
@@ -1301,11 +1362,11 @@ hipError_t run_add(const Key& k, const uint32_t* x, const uint32_t* y, uint32_t*
   hipLaunchKernelGGL((k_add<C, G>), dim3(grid_of(N, G)), dim3(kSlBlock), (size_t)(C * G) * (kSlBlock / G) * 4, s, k, x, y, out, N);
   return hipGetLastError();
 }
-template <int C, int G>
-hipError_t run_powm(const Key& k, const uint32_t* x, const uint32_t* e, int ew, uint32_t* out, long long N,
+template <int C, int G, class XS>
+hipError_t run_powm(const Key& k, const uint32_t* x, XS xs, uint32_t* out, long long N, unsigned long long* bad,
                     hipStream_t s) {
-  hipLaunchKernelGGL((k_powm<C, G>), dim3(grid_of(N, G)), dim3(kSlBlock), (size_t)(2 * C * G) * (kSlBlock / G) * 4, s, k, x, e, ew,
-                     out, N);
+  hipLaunchKernelGGL((k_powm<C, G, XS>), dim3(grid_of(N, G)), dim3(kSlBlock), (size_t)(2 * C * G) * (kSlBlock / G) * 4, s, k, x,
+                     xs, out, N, bad);
   return hipGetLastError();
 }
 template <int C, int G>
@@ -1401,12 +1462,34 @@ hipError_t sl_add(const Key& k, int C, const uint32_t* x, const uint32_t* y, uin
                   hipStream_t s) {
   SL_DISPATCH(2 * k.d.ln, C, (run_add<CC, GG>(k, x, y, out, N, s)))
 }
+template <class XS>
+hipError_t sl_powm_x(const Key& k, int C, const uint32_t* x, XS xs, uint32_t* out, long long N,
+                     unsigned long long* bad, hipStream_t s) {
+  if (table28_for(k, C)) {
+    SL_DISPATCH(2 * k.d.ln, C, (run_powm28<CC, GG, XS>(k, x, xs, out, N, bad, s)))
+  }
+  SL_DISPATCH(2 * k.d.ln, C, (run_powm<CC, GG, XS>(k, x, xs, out, N, bad, s)))
+}
 hipError_t sl_powm(const Key& k, int C, const uint32_t* x, const uint32_t* e, int ew, uint32_t* out, long long N,
                    hipStream_t s) {
-  if (table28_for(k, C)) {
-    SL_DISPATCH(2 * k.d.ln, C, (run_powm28<CC, GG>(k, x, e, ew, out, N, s)))
-  }
-  SL_DISPATCH(2 * k.d.ln, C, (run_powm<CC, GG>(k, x, e, ew, out, N, s)))
+  return sl_powm_x(k, C, x, ExpWords{e, ew}, out, N, nullptr, s);
+}
+hipError_t sl_powm_abs64(const Key& k, int C, const uint32_t* x, const long long* y, uint32_t* out, long long N,
+                         unsigned long long* bad, hipStream_t s) {
+  return sl_powm_x(k, C, x, ExpAbs64{y}, out, N, bad, s);
+}
+hipError_t sl_powm_pow2(const Key& k, int C, const uint32_t* x, const long long* y, uint32_t* out, long long N,
+                        unsigned long long* bad, hipStream_t s) {
+  return sl_powm_x(k, C, x, ExpPow2{y}, out, N, bad, s);
+}
+hipError_t sl_powm_shift(const Key& k, int C, const uint32_t* x, const long long* own, const long long* other,
+                         uint32_t* out, long long N, unsigned long long* bad, hipStream_t s) {
+  return sl_powm_x(k, C, x, ExpShift{own, other}, out, N, bad, s);
+}
+hipError_t sl_fxp_add(const Key& k, int C, const uint32_t* x, const long long* xe, const uint32_t* y,
+                      const long long* ye, uint32_t* out, long long N, unsigned long long* bad, hipStream_t s) {
+  if (!table28_for(k, C)) return hipErrorNotSupported;
+  SL_DISPATCH(2 * k.d.ln, C, (run_fxp_add28<CC, GG>(k, x, xe, y, ye, out, N, bad, s)))
 }
 hipError_t sl_matmul(const Key& k, int C, const uint32_t* X, const long long* xe, const long long* ym,
                      const long long* ye, uint32_t* zpos, uint32_t* zneg, long long* ze, int u, int v, int w,

@@ -84,6 +84,80 @@ __device__ __forceinline__ int table_window(const efl_pl_key& d) {
   return d.table_window > 0 ? d.table_window : d.group_size;
 }
 
+// ---- per-element exponents of the powm kernels (PaillierMulScalar / PaillierMulExp2) ----------
+// `xs.at(i)` gives element i's exponent: ok (false -> the op's InvalidArgument for that element),
+// bits (bit length; 0 -> x^0 = 1) and bit(b). The kernels run left to right: for b = bits-2 .. 0,
+// one squaring, then a multiply by x when bit(b) is set.
+//
+// Shifts (2^y) are capped: the reference's mpz_mul_2exp(1, y) + mpz_powm (paillier.cc:724-732)
+// does y squarings too, so a y far past any fixed-point exponent difference (fp64 spans ~2,200)
+// is hours of work there; here y > kMaxShift is reported like a negative y instead of occupying a
+// wave for minutes.
+constexpr long long kMaxShift = 1ll << 16;
+
+// |e| as `ew` little-endian 32-bit words per element (efl_pl_powm)
+struct ExpWords {
+  const uint32_t* e;
+  int ew;
+  struct El {
+    const uint32_t* p;
+    int nbits;
+    bool ok;
+    __device__ __forceinline__ int bits() const { return nbits; }
+    __device__ __forceinline__ bool bit(int b) const { return (p[b >> 5] >> (b & 31)) & 1u; }
+  };
+  __device__ __forceinline__ El at(long long i) const {
+    const uint32_t* p = e + i * ew;
+    int nb = 0;
+    for (int w = ew - 1; w >= 0; --w)
+      if (p[w]) { nb = w * 32 + 32 - __clz(p[w]); break; }
+    return El{p, nb, true};
+  }
+};
+
+// |y| of an int64 scalar (PaillierMulScalar<int64>: mpz_set_sll, then the sign picks x or x^-1)
+struct ExpAbs64 {
+  const long long* y;
+  struct El {
+    uint64_t v;
+    bool ok;
+    __device__ __forceinline__ int bits() const { return v ? 64 - __clzll(v) : 0; }
+    __device__ __forceinline__ bool bit(int b) const { return (v >> b) & 1ull; }
+  };
+  __device__ __forceinline__ El at(long long i) const {
+    const long long s = y[i];
+    return El{s < 0 ? 0ull - (uint64_t)s : (uint64_t)s, true};
+  }
+};
+
+// 2^y (PaillierMulExp2: y squarings, no multiply); y < 0 or y > kMaxShift -> not ok
+struct ExpPow2 {
+  const long long* y;
+  struct El {
+    long long s;
+    bool ok;
+    __device__ __forceinline__ int bits() const { return (int)s + 1; }
+    __device__ __forceinline__ bool bit(int) const { return false; }
+  };
+  __device__ __forceinline__ El at(long long i) const {
+    const long long s = y[i];
+    return El{s, s >= 0 && s <= kMaxShift};
+  }
+};
+
+// 2^(own - min(own, other)): one side of FixedPointTensor.__add__'s exponent alignment
+// (paillier.py:119-132: dl = max(d, 0), dr = |min(d, 0)|, d = self.exponent - another.exponent)
+struct ExpShift {
+  const long long* own;
+  const long long* other;
+  __device__ __forceinline__ ExpPow2::El at(long long i) const {
+    const long long a = own[i], b = other[i];
+    if (a <= b) return ExpPow2::El{0, true};
+    const uint64_t d = (uint64_t)a - (uint64_t)b;
+    return ExpPow2::El{d <= (uint64_t)kMaxShift ? (long long)d : 0, d <= (uint64_t)kMaxShift};
+  }
+};
+
 // Sliced kernels (paillier_sliced.hip): one number over L/C lanes of C limbs. L = limbs of the
 // modulus the op works in (2*ln for n^2 ops, ln for decryption's p^2 / q^2).
 bool sliced_available(int L, int C);
@@ -95,6 +169,18 @@ hipError_t sl_add(const Key& k, int C, const uint32_t* x, const uint32_t* y, uin
                   hipStream_t s);
 hipError_t sl_powm(const Key& k, int C, const uint32_t* x, const uint32_t* e, int ew, uint32_t* out, long long N,
                    hipStream_t s);
+// the same exponentiation with the exponent read from an int64 tensor: |y| (MulScalar) or 2^y
+// (MulExp2); elements whose exponent is not ok get z = 0 and their index atomically min'ed into bad
+hipError_t sl_powm_abs64(const Key& k, int C, const uint32_t* x, const long long* y, uint32_t* out, long long N,
+                         unsigned long long* bad, hipStream_t s);
+hipError_t sl_powm_pow2(const Key& k, int C, const uint32_t* x, const long long* y, uint32_t* out, long long N,
+                        unsigned long long* bad, hipStream_t s);
+hipError_t sl_powm_shift(const Key& k, int C, const uint32_t* x, const long long* own, const long long* other,
+                         uint32_t* out, long long N, unsigned long long* bad, hipStream_t s);
+// z = x^(2^(xe - m)) y^(2^(ye - m)) mod n^2, m = min(xe, ye): FixedPointTensor.__add__ in one launch
+// (radix-2^28 family only: hipErrorNotSupported otherwise, and the caller composes powm + add)
+hipError_t sl_fxp_add(const Key& k, int C, const uint32_t* x, const long long* xe, const uint32_t* y,
+                      const long long* ye, uint32_t* out, long long N, unsigned long long* bad, hipStream_t s);
 hipError_t sl_matmul(const Key& k, int C, const uint32_t* X, const long long* xe, const long long* ym,
                      const long long* ye, uint32_t* zpos, uint32_t* zneg, long long* ze, int u, int v, int w,
                      hipStream_t s);

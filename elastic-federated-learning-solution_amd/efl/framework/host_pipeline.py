@@ -67,7 +67,21 @@ class PinnedCodecPipeline:
 
     def _run(self, srcs, dsts, kernel, in_dtypes, out_dtypes):
         """srcs: host 1-D tensors (same numel); dsts: pinned host 1-D outputs. kernel(ins, outs,
-        n, stream_handle) enqueues the codec on the compute stream."""
+        n, stream_handle) enqueues the codec on the compute stream.
+
+        The pipeline's streams first wait for the caller's current stream: the device slots are
+        allocated lazily on it, and the caching allocator may hand them a block just freed there
+        while a kernel on that stream still reads it. The body runs without autograd: the cached
+        slots and staging chunks must never join a caller's graph (an activation that requires grad
+        reaches here through FixedPointHook.pre_send)."""
+        cur = torch.cuda.current_stream(self.device)
+        self.s_in.wait_stream(cur)
+        self.s_run.wait_stream(cur)
+        self.s_out.wait_stream(cur)
+        with torch.no_grad():
+            self._run_chunks(srcs, dsts, kernel, in_dtypes, out_dtypes)
+
+    def _run_chunks(self, srcs, dsts, kernel, in_dtypes, out_dtypes):
         n = srcs[0].numel()
         ev_in = [torch.cuda.Event() for _ in range(self.nbuf)]
         ev_run = [torch.cuda.Event() for _ in range(self.nbuf)]
@@ -111,7 +125,7 @@ class PinnedCodecPipeline:
         if x.is_cuda:
             raise errors.InvalidArgumentError("PinnedCodecPipeline.encode takes a host tensor")
         code = _lib.dt_code(x.dtype)
-        flat = x.contiguous().reshape(-1)
+        flat = x.detach().contiguous().reshape(-1)
         if out is None:
             out = (torch.empty(flat.numel(), dtype=torch.int64, pin_memory=True),
                    torch.empty(flat.numel(), dtype=torch.int64, pin_memory=True))
@@ -137,8 +151,8 @@ class PinnedCodecPipeline:
         dtype = _lib.to_torch_dtype(dtype)
         code = _lib.dt_code(dtype)
         ftz = _lib.flush_denormal() if flush_denormal is None else bool(flush_denormal)
-        Mf = mantissa.contiguous().reshape(-1)
-        Ef = exponent.contiguous().reshape(-1)
+        Mf = mantissa.detach().contiguous().reshape(-1)
+        Ef = exponent.detach().contiguous().reshape(-1)
         y = out if out is not None else torch.empty(Mf.numel(), dtype=dtype, pin_memory=True)
         yf = y.reshape(-1)
         raw = _lib.raw()

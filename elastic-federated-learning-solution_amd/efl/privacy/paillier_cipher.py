@@ -61,6 +61,10 @@ for _name, _args in {
     "efl_pl_to_int64": [_vp, _i32, _vp, _vp, _i64, _vp],
     "efl_pl_invert": [_vp, _PK, _vp, _vp, _i64, _vp, _vp],
     "efl_pl_matmul": [_vp, _PK, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _vp],
+    "efl_pl_mul_exp2": [_vp, _PK, _vp, _vp, _vp, _i64, _vp, _vp],
+    "efl_pl_mul_scalar": [_vp, _PK, _vp, _vp, _vp, _i64, _vp, _vp],
+    "efl_pl_mul_scalar_big": [_vp, _PK, _vp, _vp, _i32, _vp, _vp, _i64, _vp, _vp],
+    "efl_pl_fxp_add": [_vp, _PK, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp],
     "efl_pl_tune": [_i32, _i32, _i32],
 }.items():
     getattr(_lib, _name).argtypes = _args
@@ -709,18 +713,6 @@ class PaillierKeypair(object):
                                        x.numel(), _stream(k.device)))
         return CipherTensor(out, x.shape, k)
 
-    def _powm(self, x: CipherTensor, exps: list[int]) -> CipherTensor:
-        k = self.key
-        N = x.numel()
-        emax = max((e.bit_length() for e in exps), default=1)
-        ew = max(1, (emax + 31) // 32)
-        arr = np.stack([_limbs(e, ew) for e in exps]) if N else np.zeros((0, ew), "<u4")
-        e_dev = torch.from_numpy(arr.view(np.int32)).to(k.device)
-        out = torch.empty_like(x.limbs)
-        _efl_lib.check(_lib.efl_pl_powm(*k.args(), x.limbs.data_ptr(), e_dev.data_ptr(), ew, out.data_ptr(), N,
-                                        _stream(k.device)))
-        return CipherTensor(out, x.shape, k)
-
     def invert(self, x):
         """PaillierInvert: x^-1 mod n^2 (paillier.cc:267-285, 721-797)."""
         k = self.key
@@ -735,18 +727,34 @@ class PaillierKeypair(object):
         return CipherTensor(out, x.shape, k)
 
     def mul_scalar(self, x, scalar):
-        """PaillierMulScalar: x^y mod n^2; for y < 0 the reference computes (x^-1)^|y|
-        (paillier.cc:180-265), the same element as (x^|y|)^-1, which is what runs here."""
+        """PaillierMulScalar (paillier.cc:180-265, :616-678): z = x^y mod n^2. T = int32/int64
+        (torch/numpy integers, Python ints of int64 range): efl_pl_mul_scalar, which computes
+        x^|y| and inverts it where y < 0 — the element the reference forms as (x^-1)^|y|. T = string
+        (str / bytes / HexTensor, or Python ints wider than int64): signed hex big integers parsed
+        on the GPU as mpz_init_set_str(op, y, 16) does (:239-248), then efl_pl_mul_scalar_big.
+        x and y broadcast against each other first (paillier.py:81-85)."""
+        k = self.key
         x = self._cipher(x)
-        ys = _scalar_list(scalar, x.shape)
-        x, ys = _broadcast_scalar(x, ys)
-        z = self._powm(x, [abs(y) for y in ys])
-        negs = [i for i, y in enumerate(ys) if y < 0]
-        if negs:
-            idx = torch.tensor(negs, dtype=torch.int64, device=z.limbs.device)
-            zi = self.invert(CipherTensor(z.limbs[idx].contiguous(), (len(negs),), z.key))
-            z.limbs[idx] = zi.limbs
-        return z
+        y = _scalar_operand(scalar, k.device)
+        shape = _broadcast_shape(x.shape, y.shape)
+        x = _expand(x, shape)
+        N = x.numel()
+        out = torch.empty_like(x.limbs)
+        bad = torch.empty(1, dtype=torch.int64, device=k.device)
+        if isinstance(y, HexTensor):
+            y = _expand_hex(y, shape)
+            L = max(1, _hex_words(y))
+            mag, neg = hex_to_limbs(y, L, k.device, signed=True)
+            _efl_lib.check(_lib.efl_pl_mul_scalar_big(*k.args(), x.limbs.data_ptr(), mag.data_ptr(), L, neg.data_ptr(),
+                                                      out.data_ptr(), N, bad.data_ptr(), _stream(k.device)))
+        else:
+            y = y.expand(shape).reshape(-1).contiguous()
+            _efl_lib.check(_lib.efl_pl_mul_scalar(*k.args(), x.limbs.data_ptr(), y.data_ptr(), out.data_ptr(), N,
+                                                  bad.data_ptr(), _stream(k.device)))
+        b = int(bad.item())
+        if b >= 0:
+            raise errors.InvalidArgumentError(f"element {b} has no inverse mod n^2 (a negative scalar needs x^-1)")
+        return CipherTensor(out, shape, k)
 
     def matmul(self, xm, xe, ym, ye):
         """PaillierMatmul (paillier.cc:915-1053): ciphertext [u, v] x plaintext fixed-point [v, w]
@@ -781,13 +789,99 @@ class PaillierKeypair(object):
         return CipherTensor(zpos, (u, w), k), ze
 
     def mul_exp2(self, x, exp):
-        """PaillierMulExp2: x^(2^y) mod n^2, y >= 0 (paillier.cc:615-719)."""
+        """PaillierMulExp2 (paillier.cc:680-751): z = x^(2^y) mod n^2, y int32/int64 >= 0, y
+        squarings per element on the GPU (efl_pl_mul_exp2). x and y broadcast first (paillier.py:87-91)."""
+        k = self.key
         x = self._cipher(x)
-        ys = _scalar_list(exp, x.shape)
-        x, ys = _broadcast_scalar(x, ys)
-        if any(y < 0 for y in ys):
-            raise errors.InvalidArgumentError("y should be a positive tensor.")
-        return self._powm(x, [1 << y for y in ys])
+        y = _scalar_operand(exp, k.device)
+        if isinstance(y, HexTensor):
+            raise errors.InvalidArgumentError("PaillierMulExp2: y must be int32 or int64")
+        shape = _broadcast_shape(x.shape, y.shape)
+        x = _expand(x, shape)
+        y = y.expand(shape).reshape(-1).contiguous()
+        out = torch.empty_like(x.limbs)
+        bad = torch.empty(1, dtype=torch.int64, device=k.device)
+        _efl_lib.check(_lib.efl_pl_mul_exp2(*k.args(), x.limbs.data_ptr(), y.data_ptr(), out.data_ptr(), x.numel(),
+                                            bad.data_ptr(), _stream(k.device)))
+        b = int(bad.item())
+        if b >= 0:
+            _raise_shift(int(y[b].item()))
+        return CipherTensor(out, shape, k)
+
+    def shift_add(self, x, x_exponent, y, y_exponent):
+        """The ciphertext half of FixedPointTensor.__add__ (paillier.py:119-132):
+        (x << dl) + (y << dr) = x^(2^(xe - m)) * y^(2^(ye - m)) mod n^2, m = min(xe, ye), as ONE
+        launch (efl_pl_fxp_add) instead of two PaillierMulExp2 and a PaillierAdd; the same ciphertext
+        bits. Everything broadcasts to one shape. Returns (CipherTensor, m)."""
+        k = self.key
+        x, y = self._cipher(x), self._cipher(y)
+        xe = _efl_lib.as_tensor(x_exponent).to(k.device, torch.int64)
+        ye = _efl_lib.as_tensor(y_exponent).to(k.device, torch.int64)
+        shape = _broadcast_shape(_broadcast_shape(x.shape, y.shape), _broadcast_shape(tuple(xe.shape), tuple(ye.shape)))
+        x, y = _expand(x, shape), _expand(y, shape)
+        xe = xe.expand(shape).reshape(-1).contiguous()
+        ye = ye.expand(shape).reshape(-1).contiguous()
+        out = torch.empty_like(x.limbs)
+        bad = torch.empty(1, dtype=torch.int64, device=k.device)
+        _efl_lib.check(_lib.efl_pl_fxp_add(*k.args(), x.limbs.data_ptr(), xe.data_ptr(), y.limbs.data_ptr(),
+                                           ye.data_ptr(), out.data_ptr(), x.numel(), bad.data_ptr(), _stream(k.device)))
+        b = int(bad.item())
+        if b >= 0:
+            _raise_shift(abs(int(xe[b].item()) - int(ye[b].item())))
+        return CipherTensor(out, shape, k), torch.minimum(xe, ye).reshape(shape)
+
+
+MAX_SHIFT = 1 << 16   # pl_common.h kMaxShift
+
+
+def _raise_shift(y: int):
+    if y < 0:
+        raise errors.InvalidArgumentError("y should be a positive tensor.")
+    raise errors.UnimplementedError(f"shift by 2^{y}: more than {MAX_SHIFT} squarings per element are not "
+                                    "supported on the GPU (DESIGN.md §5)")
+
+
+def _scalar_operand(s, device):
+    """The y operand of PaillierMulScalar / PaillierMulExp2 (TF T = int32/int64/string): an int64
+    tensor on `device`, or a HexTensor of signed hex integers for the string variant (and for Python
+    ints beyond int64, which only the string variant can carry)."""
+    if isinstance(s, HexTensor):
+        return s
+    if isinstance(s, torch.Tensor):
+        if s.dtype.is_floating_point or s.dtype.is_complex or s.dtype == torch.bool:
+            raise errors.InvalidArgumentError(f"scalar dtype must be int32, int64 or string, got {s.dtype}")
+        return s.to(device, torch.int64)
+    if isinstance(s, (str, bytes, bytearray)):
+        return HexTensor.from_strings([s], shape=())
+    a = np.asarray(s) if not isinstance(s, np.ndarray) else s
+    if a.dtype.kind in "iu":
+        if a.dtype == np.uint64 and a.size and int(a.max()) >= 1 << 63:
+            return HexTensor.from_ints([int(v) for v in a.reshape(-1)], a.shape)
+        return torch.from_numpy(np.ascontiguousarray(a, np.int64)).to(device)
+    if a.dtype.kind in "USO":
+        flat = a.reshape(-1).tolist()
+        if all(isinstance(v, (int, np.integer)) and not isinstance(v, bool) for v in flat):
+            if all(-(1 << 63) <= int(v) < (1 << 63) for v in flat):
+                return torch.tensor([int(v) for v in flat], dtype=torch.int64).reshape(a.shape).to(device)
+            return HexTensor.from_ints([int(v) for v in flat], a.shape)
+        if all(isinstance(v, (str, bytes, bytearray, np.str_, np.bytes_)) for v in flat):
+            return HexTensor.from_strings(np.array(flat, dtype=object).reshape(a.shape))
+    raise errors.InvalidArgumentError(f"scalar must be int32, int64 or string, got {a.dtype}")
+
+
+def _hex_words(hx: HexTensor) -> int:
+    """32-bit words that hold the widest text's magnitude (8 hex digits per word)."""
+    offs = hx.offs
+    if hx.numel() == 0:
+        return 1
+    return int(((offs[1:] - offs[:-1]).max() + 7) // 8)
+
+
+def _expand_hex(hx: HexTensor, shape) -> HexTensor:
+    if hx.shape == tuple(shape):
+        return hx
+    idx = np.broadcast_to(np.arange(hx.numel()).reshape(hx.shape), shape).reshape(-1)
+    return hx.take(idx, shape)
 
 
 def _counter_runs(idx: np.ndarray):
@@ -800,13 +894,6 @@ def _counter_runs(idx: np.ndarray):
             runs.append((j0, j, int(idx[j0])))
             j0 = j
     return runs
-
-
-def _scalar_list(s, shape):
-    if isinstance(s, torch.Tensor):
-        return [int(v) for v in s.reshape(-1).cpu().tolist()], tuple(s.shape)
-    a = np.asarray(s)
-    return [int(v) for v in a.reshape(-1).tolist()], a.shape
 
 
 def _broadcast_shape(a, b):
@@ -825,14 +912,6 @@ def _expand(x: CipherTensor, shape) -> CipherTensor:
     return CipherTensor(x.limbs[idx].contiguous(), shape, x.key)
 
 
-def _broadcast_scalar(x: CipherTensor, ys_shape):
-    ys, yshape = ys_shape
-    shape = _broadcast_shape(x.shape, yshape)
-    x = _expand(x, shape)
-    ys = np.broadcast_to(np.array(ys, dtype=object).reshape(yshape), shape).reshape(-1).tolist()
-    return x, [int(v) for v in ys]
-
-
 # ----------------------------------------------------------------------------------------------
 # FixedPointTensor arithmetic with encrypted mantissas (paillier.py:116-145)
 # ----------------------------------------------------------------------------------------------
@@ -844,16 +923,12 @@ def _fp_encode(v):
 
 def fixedpoint_add(self, another):
     """FixedPointTensor.__add__ (paillier.py:116-133): align exponents with mul_exp2 shifts, then
-    add in ciphertext space; a plaintext side is encrypted with the other side's keypair."""
+    add in ciphertext space; a plaintext side is encrypted with the other side's keypair. The shifts
+    and the add run as one launch (PaillierKeypair.shift_add): bit-identical to
+    (self_m << dl) + (another_m << dr)."""
     from efl.privacy.paillier import FixedPointTensor
     another = _fp_encode(another)
     se, ae = _efl_lib.as_tensor(self.exponent), _efl_lib.as_tensor(another.exponent)
-    dev = se.device if se.is_cuda else ae.device
-    se, ae = se.to(dev), ae.to(dev)
-    exponent = torch.minimum(se, ae)
-    d = se - ae
-    dl = torch.clamp(d, min=0)
-    dr = torch.abs(torch.clamp(d, max=0))
     if not isinstance(self.mantissa, PaillierTensor):
         self_m = another.mantissa.keypair.encrypt(self.mantissa)
         another_m = another.mantissa
@@ -862,8 +937,9 @@ def fixedpoint_add(self, another):
         another_m = self.mantissa.keypair.encrypt(another.mantissa)
     else:
         self_m, another_m = self.mantissa, another.mantissa
-    mantissa = (self_m << dl) + (another_m << dr)
-    return FixedPointTensor(mantissa, exponent)
+    kp = self_m.keypair
+    mantissa, exponent = kp.shift_add(self_m.tensor, se, another_m.tensor, ae)
+    return FixedPointTensor(PaillierTensor(kp, mantissa), exponent)
 
 
 def fixedpoint_mul(self, another):

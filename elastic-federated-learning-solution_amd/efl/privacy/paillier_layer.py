@@ -205,13 +205,15 @@ class PaillierPassiveWeight(PaillierPassiveDense):
         return x * fw
 
     def cipher_grad_w(self, x, dy):
+        """dw = the column sums of [x] * encode(dy). The reference adds the rows one at a time in a
+        tf.while_loop (:297-310): acc + row aligns the two exponents to their minimum and multiplies,
+        so after all rows the mantissa is prod_r [x dy]_rc^(2^(e_rc - min_r e_rc)) mod n^2 with
+        exponent min_r e_rc, whatever the order. That is exactly a PaillierMatmul of [x dy]^T by a
+        column of ones with exponent 0 (paillier.cc:915-1053): one Straus multi-exponentiation per
+        column (max_r d squarings instead of sum_r d), one launch instead of rows - 1 adds; the same
+        ciphertext bits (tests/test_paillier_layer_gpu.py checks them against the sequential sum)."""
         dw = x * fixedpoint_encode(dy, decrease_precision=True)
-        m = dw.mantissa.tensor
-        rows = m.shape[0]
-        acc = FixedPointTensor(PaillierTensor(self.keypair, _row(m, 0)), dw.exponent[0])
-        for i in range(1, rows):   # the reference's tf.while_loop over rows (:295-303)
-            acc = acc + FixedPointTensor(PaillierTensor(self.keypair, _row(m, i)), dw.exponent[i])
-        return acc
+        return column_sum(self.keypair, dw)
 
     def plain_grad_x(self, dy, w):
         return dy * w
@@ -235,10 +237,31 @@ def _device_of(inputs):
     return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
 
 
-def _row(c, i):
+def column_sum(keypair, fp):
+    """sum over rows of a FixedPointTensor with an encrypted [rows, cols] mantissa -> [cols]
+    (PaillierPassiveWeight's gradient reduction, paillier_layer.py:297-310), as one
+    PaillierMatmul by ones: [cols, rows] x [rows, 1]."""
+    m = fp.mantissa.tensor
+    rows, cols = m.shape
+    e = torch.as_tensor(fp.exponent).to(m.limbs.device, torch.int64)
+    ones = torch.ones((rows, 1), dtype=torch.int64, device=m.limbs.device)
+    zm, ze = keypair.matmul(m.transpose(), e.t().contiguous(), ones, torch.zeros_like(ones))
+    return FixedPointTensor(PaillierTensor(keypair, zm.reshape((cols,))), ze.reshape(cols))
+
+
+def sequential_column_sum(keypair, fp):
+    """The reference's row-by-row loop (paillier_layer.py:297-310) over FixedPointTensor.__add__:
+    the definition column_sum is tested against."""
     from efl.privacy.paillier_cipher import CipherTensor
-    r, cols = c.shape
-    return CipherTensor(c.limbs[i * cols:(i + 1) * cols].contiguous(), (cols,), c.key)
+    m = fp.mantissa.tensor
+    rows, cols = m.shape
+
+    def row(i):
+        return CipherTensor(m.limbs[i * cols:(i + 1) * cols].contiguous(), (cols,), m.key)
+    acc = FixedPointTensor(PaillierTensor(keypair, row(0)), fp.exponent[0])
+    for i in range(1, rows):
+        acc = acc + FixedPointTensor(PaillierTensor(keypair, row(i)), fp.exponent[i])
+    return acc
 
 
 # ----------------------------------------------------------------------------------------------

@@ -227,6 +227,36 @@ int efl_pl_add(const void* key_block, const efl_pl_key* key, const uint32_t* x, 
 int efl_pl_powm(const void* key_block, const efl_pl_key* key, const uint32_t* x, const uint32_t* exps,
                 int exp_words, uint32_t* z, int64_t n, void* stream);
 
+/* PaillierMulExp2<int64> (paillier.cc:680-751; the int32 variant after widening): z = x^(2^y) mod
+ * n^2, y squarings per element, no host-side exponent. y < 0 is the op's InvalidArgument "y should
+ * be a positive tensor." (:724-726, :740-742); so is y > 65536 here (the reference
+ * would spend hours there). bad (device, one int64) <- -1, or the smallest such index (its z is 0). */
+int efl_pl_mul_exp2(const void* key_block, const efl_pl_key* key, const uint32_t* x, const int64_t* y,
+                    uint32_t* z, int64_t n, int64_t* bad, void* stream);
+
+/* PaillierMulScalar<int64> (paillier.cc:197-237, :616-678; int32 after widening): z = x^|y| mod n^2,
+ * then inverted mod n^2 where y < 0 — the element the reference computes as (x^-1)^|y|. One powm
+ * launch plus one in-place inversion launch restricted to the negative scalars. bad <- -1, or the
+ * smallest index with y < 0 whose x has no inverse mod n^2 (its z is 0). */
+int efl_pl_mul_scalar(const void* key_block, const efl_pl_key* key, const uint32_t* x, const int64_t* y,
+                      uint32_t* z, int64_t n, int64_t* bad, void* stream);
+
+/* PaillierMulScalar<string> (paillier.cc:239-248: mpz_init_set_str(op, y, 16), signed big-integer
+ * scalars): |y| as y_words little-endian 32-bit words per element plus sign bytes (1 = negative),
+ * as efl_hex_parse produces them from the hex text; y_negative NULL = all non-negative. Same
+ * result and bad convention as efl_pl_mul_scalar. */
+int efl_pl_mul_scalar_big(const void* key_block, const efl_pl_key* key, const uint32_t* x,
+                          const uint32_t* y_magnitude, int y_words, const int8_t* y_negative, uint32_t* z,
+                          int64_t n, int64_t* bad, void* stream);
+
+/* FixedPointTensor.__add__ with encrypted mantissas (python/efl/privacy/paillier.py:116-133):
+ * z = x^(2^(xe - m)) * y^(2^(ye - m)) mod n^2, m = min(xe, ye) (the caller keeps m as the exponent):
+ * the reference's (x << dl) + (y << dr), i.e. two PaillierMulExp2 and one PaillierAdd, fused into
+ * one launch. |xe - ye| > 65536 -> bad as in efl_pl_mul_exp2. */
+int efl_pl_fxp_add(const void* key_block, const efl_pl_key* key, const uint32_t* x, const int64_t* x_exponent,
+                   const uint32_t* y, const int64_t* y_exponent, uint32_t* z, int64_t n, int64_t* bad,
+                   void* stream);
+
 /* PaillierInvert (paillier.cc:267-285, :721-797): z = x^-1 mod n^2 (Pornin's batched binary GCD,
  * "Optimized Binary GCD for Modular Inversion", 2020, on the GPU). bad <- -1, or
  * the first index without an inverse (its z is 0). */

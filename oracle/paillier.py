@@ -156,6 +156,30 @@ def invert(kp, x):                                        # paillier.cc:267-285
     return pow(x, -1, kp.n2)
 
 
+def mul_scalar_hex(kp, x, y: str):                        # paillier.cc:239-248 (T = string)
+    """mpz_init_set_str(op, y, 16): the scalar text is a signed hex integer."""
+    return mul_scalar(kp, x, int(y, 16))
+
+
+def fixedpoint_add(kp, xm, xe: int, ym, ye: int):         # python/efl/privacy/paillier.py:116-133
+    """FixedPointTensor.__add__ of two encrypted mantissas, element-wise: d = xe - ye,
+    dl = max(d, 0), dr = |min(d, 0)|; mantissa = (x << dl) + (y << dr) = PaillierAdd of two
+    PaillierMulExp2; exponent = min(xe, ye)."""
+    d = xe - ye
+    return add(kp, mul_exp2(kp, xm, max(d, 0)), mul_exp2(kp, ym, abs(min(d, 0)))), min(xe, ye)
+
+
+def column_sum(kp, xm, xe):                               # python/efl/privacy/paillier_layer.py:297-310
+    """The PaillierPassiveWeight gradient reduction: the rows of an encrypted FixedPointTensor
+    ([rows][cols] ciphertexts and exponents) added one at a time, as the reference's
+    tf.while_loop does."""
+    acc_m, acc_e = list(xm[0]), list(xe[0])
+    for r in range(1, len(xm)):
+        for c in range(len(acc_m)):
+            acc_m[c], acc_e[c] = fixedpoint_add(kp, acc_m[c], acc_e[c], xm[r][c], xe[r][c])
+    return acc_m, acc_e
+
+
 def matmul(kp, xm, xe, ym, ye):
     """PaillierMatmul (paillier.cc:941-1051): xm [u][v] ciphertexts, xe/ym/ye int matrices.
     z[i][k] = prod_j (xm[i][j]^ym[j][k])^(2^(xe+ye - min)) ; z_exp = min_j (xe[i][j] + ye[j][k])."""

@@ -39,3 +39,25 @@ def test_fixed_point_hook_over_grpc():
     finally:
         leader.shutdown()
         follower.shutdown()
+
+
+def test_pipeline_slots_never_join_autograd():
+    """a host activation that requires grad goes through the pinned pipeline (as
+    FixedPointHook.pre_send sends it) twice; the cached device slots and pinned staging chunks stay
+    plain buffers (no grad_fn chain across steps), and the bits equal the oracle."""
+    import efl
+    from efl.framework.host_pipeline import PinnedCodecPipeline
+    pipe = PinnedCodecPipeline(chunk_elems=1 << 12)
+    x = torch.randn(3 * 4096 + 17, generator=torch.Generator().manual_seed(5)).requires_grad_(True)
+    for _ in range(2):
+        M, E = pipe.encode(x)                                  # pageable source: staged chunks
+        Mp, Ep = pipe.encode(x.detach().pin_memory())          # pinned source
+        y = pipe.decode(M, E)
+    for t in list(pipe._slots.values()) + list(pipe._stage.values()):
+        assert not t.requires_grad and t.grad_fn is None
+    assert not M.requires_grad and not y.requires_grad
+    Mo, Eo = fxp.encode(x.detach().numpy())
+    assert np.array_equal(M.numpy(), Mo) and np.array_equal(E.numpy(), Eo)
+    assert np.array_equal(Mp.numpy(), Mo) and np.array_equal(Ep.numpy(), Eo)
+    assert np.array_equal(y.numpy().view(np.uint32), fxp.decode(Mo, Eo).view(np.uint32))
+    assert efl.lib.flush_denormal() in (True, False)

@@ -10,7 +10,10 @@ cipher op and communicator call synchronised and timed (exclusive times: a matmu
 add count under invert / add, a send's hex formatting under send), and how many elements each op
 processed. Prints one JSON line per party.
 
-    python tools/bench_layer.py [--steps 3] [--warmup 1]
+    python tools/bench_layer.py [--steps 3] [--warmup 1] [--kind dense|weight]
+
+--kind weight runs efl.paillier.{sender,recver}.weight instead (paillier_layer.py:209-360): an
+element-wise [256, 128] kernel, whose receiver reduces the gradient over rows (one matmul launch).
 """
 import argparse
 import collections
@@ -82,7 +85,7 @@ def _numel(x):
     return 0
 
 
-def party(role, my, peer, q, steps, warmup):
+def party(role, my, peer, q, steps, warmup, kind):
     try:
         import torch
         import efl
@@ -96,16 +99,23 @@ def party(role, my, peer, q, steps, warmup):
         efl.paillier.Hook(kp, c, Role.SENDER if role == "follower" else Role.RECEIVER, "k",
                           n_bytes=N_BYTES).after_create_session()
         g = torch.Generator().manual_seed(0)
-        x = torch.randn(ROWS, FEATURES, generator=g).cuda()
+        feats = FEATURES if kind == "dense" else UNITS
+        x = torch.randn(ROWS, feats, generator=g).cuda()
         dy = torch.randn(ROWS, UNITS, generator=g).cuda()
 
         def step():
             if role == "follower":     # sender: owns the key and the activations
                 xi = x.clone().requires_grad_(True)
-                out, _ = efl.paillier.sender.dense(xi, kp, c, "l1", UNITS, seed=1)
+                if kind == "dense":
+                    out, _ = efl.paillier.sender.dense(xi, kp, c, "l1", UNITS, seed=1)
+                else:
+                    out, _ = efl.paillier.sender.weight(xi, kp, c, "l1", UNITS, seed=1)
                 out.backward(dy)
             else:                      # receiver: holds W
-                y, _ = efl.paillier.recver.dense(None, kp, c, "l1", (ROWS, FEATURES), UNITS, seed=2)
+                if kind == "dense":
+                    y, _ = efl.paillier.recver.dense(None, kp, c, "l1", (ROWS, FEATURES), UNITS, seed=2)
+                else:
+                    y, _ = efl.paillier.recver.weight(None, kp, c, "l1", UNITS, seed=2)
                 y.backward(dy)
             torch.cuda.synchronize()
             c.add_step()
@@ -119,10 +129,18 @@ def party(role, my, peer, q, steps, warmup):
 
         timer = OpTimer(torch.cuda.synchronize)
         cls = PaillierKeypair
-        for attr in ("encrypt", "decrypt", "matmul", "add", "invert", "mul_scalar"):
+        for attr in ("encrypt", "decrypt", "matmul", "add", "invert", "mul_scalar", "mul_exp2", "shift_add",
+                     "_cipher"):
             if hasattr(cls, attr):
-                timer.wrap(cls, attr, attr, (lambda self, v, *a, **k: _numel(v)) if attr != "matmul" else
+                timer.wrap(cls, attr, attr if attr != "_cipher" else "hex parse (_cipher)",
+                           (lambda self, v, *a, **k: _numel(v)) if attr != "matmul" else
                            (lambda self, xm, xe, ym, ye: int(xe.shape[0]) * int(ym.shape[1])))
+        from efl.privacy import paillier as fxp_api
+        for attr in ("fixedpoint_encode", "fixedpoint_decode"):
+            timer.wrap(fxp_api, attr, attr)
+        from efl.privacy import paillier_layer as layer_mod
+        timer.wrap(layer_mod, "fixedpoint_encode", "fixedpoint_encode")
+        timer.wrap(layer_mod, "_decrypt_decode", "decrypt+decode")
         timer.wrap(c, "_send_raw", "send (serialise, hex)", lambda name, t: _numel(t))
         timer.wrap(c, "_recv_raw", "recv (wait, parse)")
         timer.on = True
@@ -134,6 +152,7 @@ def party(role, my, peer, q, steps, warmup):
         q.put((role, {"party": "sender (key owner, x)" if role == "follower" else "receiver (W)",
                       "step_ms": round(wall * 1e3, 1), "instrumented_step_ms": round(inst * 1e3, 1),
                       "ops_ms": {k: round(v * 1e3, 2) for k, v in sorted(timer.total.items(), key=lambda kv: -kv[1])},
+                      "attributed_frac": round(sum(timer.total.values()) / inst, 3),
                       "calls": dict(timer.calls), "elements": dict(timer.elems)}, None))
     except BaseException as e:  # pragma: no cover - reported to the parent
         import traceback
@@ -144,12 +163,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--kind", choices=("dense", "weight"), default="dense")
     a = ap.parse_args()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     pl, pf = free_port(), free_port()
-    ps = [ctx.Process(target=party, args=("leader", pl, pf, q, a.steps, a.warmup)),
-          ctx.Process(target=party, args=("follower", pf, pl, q, a.steps, a.warmup))]
+    ps = [ctx.Process(target=party, args=("leader", pl, pf, q, a.steps, a.warmup, a.kind)),
+          ctx.Process(target=party, args=("follower", pf, pl, q, a.steps, a.warmup, a.kind))]
     for p in ps:
         p.start()
     out, err = {}, None
@@ -163,8 +183,9 @@ def main():
     if err:
         raise SystemExit(f"{err[0]} failed:\n{err[1]}")
     for role in ("follower", "leader"):
-        print(json.dumps({"bench": "paillier_mnist dense layer step, two processes, 1024-bit key",
-                          "shape": {"activations": [ROWS, FEATURES], "units": UNITS}, **out[role]}), flush=True)
+        print(json.dumps({"bench": f"paillier_mnist {a.kind} layer step, two processes, 1024-bit key",
+                          "shape": {"activations": [ROWS, FEATURES if a.kind == "dense" else UNITS], "units": UNITS},
+                          **out[role]}), flush=True)
 
 
 if __name__ == "__main__":
