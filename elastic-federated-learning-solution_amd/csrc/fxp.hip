@@ -341,14 +341,12 @@ __global__ __launch_bounds__(kBlock) void k_scalar(typename Op::Args a, long lon
     Op::scalar(a, i);
 }
 
-// Batched: blockIdx.y = tensor, blockIdx.x = tile of that tensor (one launch for `count`
-// tensors; BASELINE config 3). Arrays of pointers / sizes live in device memory. Same tile shape
-// as k_stream (B lanes x K units, every load of a full tile issued before the transform).
+// Batched (BASELINE config 3): tile `x` of tensor `t`, one launch for `count` tensors. Arrays of
+// pointers / sizes live in device memory (t is wave-uniform: scalar loads). Same tile shape as
+// k_stream (B lanes x K units, every load of a full tile issued before the transform).
 template <class Op, int B, int K, int NT>
-__global__ __launch_bounds__(B) void k_batched(const void* const* src, void* const* dst0,
-                                               void* const* dst1, const long long* ns,
-                                               int flag, long long tile_base) {
-  const long long t = tile_base + blockIdx.y;
+__device__ __forceinline__ void batched_tile(const void* const* src, void* const* dst0, void* const* dst1,
+                                             const long long* ns, int flag, long long t, long long x) {
   const long long n = ns[t];
   typename Op::Args a;
   if constexpr (std::is_same<typename Op::Args, EncArgs>::value) {
@@ -357,12 +355,12 @@ __global__ __launch_bounds__(B) void k_batched(const void* const* src, void* con
     a = DecArgs{(const long long*)src[t], (const long long*)dst0[t], dst1[t], flag};
   }
   const long long tile = (long long)B * K * Op::kElems;
-  const long long e0 = (long long)blockIdx.x * tile;
+  const long long e0 = x * tile;
   if (e0 >= n) return;
   // 16-B alignment of this tensor's streams decides vector vs element path (uniform branch).
   const bool vec = aligned(src[t], 16) && aligned(dst0[t], 16) && aligned(dst1[t], 16);
   const long long nunits = n / Op::kElems;
-  const long long u0 = (long long)blockIdx.x * B * K;
+  const long long u0 = x * B * K;
   if (vec) {
     typename Op::In v[K];
     if (u0 + (long long)B * K <= nunits) {
@@ -391,6 +389,26 @@ __global__ __launch_bounds__(B) void k_batched(const void* const* src, void* con
   } else {
     for (long long i = e0 + threadIdx.x; i < n && i < e0 + tile; i += B) Op::scalar(a, i);
   }
+}
+
+// 2-D grid: blockIdx.y = tensor (from tile_base), blockIdx.x = tile of that tensor.
+template <class Op, int B, int K, int NT>
+__global__ __launch_bounds__(B) void k_batched(const void* const* src, void* const* dst0,
+                                               void* const* dst1, const long long* ns,
+                                               int flag, long long tile_base) {
+  batched_tile<Op, B, K, NT>(src, dst0, dst1, ns, flag, tile_base + blockIdx.y, blockIdx.x);
+}
+
+// 1-D grid over count x gx tiles (tensor-major), XCD-aware like k_stream: workgroups are dispatched
+// round-robin over the 8 XCDs, and workgroup b takes linear tile (b % 8) * per + b / 8, so each XCD
+// streams one contiguous eighth of the tensors (and of their tiles) instead of every eighth tile.
+template <class Op, int B, int K, int NT>
+__global__ __launch_bounds__(B) void k_batched_flat(const void* const* src, void* const* dst0,
+                                                    void* const* dst1, const long long* ns, int flag,
+                                                    long long gx, long long total, long long per) {
+  const long long lin = per > 0 ? (long long)(blockIdx.x & 7u) * per + (blockIdx.x >> 3) : blockIdx.x;
+  if (lin >= total) return;
+  batched_tile<Op, B, K, NT>(src, dst0, dst1, ns, flag, lin / gx, lin % gx);
 }
 
 // Hex mantissa decode (FixedPointToFloatPointOp<string, T>, fixed_point.cc:255-257): one lane per
@@ -476,6 +494,9 @@ constexpr long long kMaxGridY = 65535;
 // step (tools/batched_probe.py, profiles/r02/batched_probe*.json); decode's shape is within noise
 std::atomic<int> g_batch_block[2] = {{kBatchB}, {kBatchB}};
 std::atomic<int> g_batch_k[2] = {{2}, {kBatchK}};
+// efl_fxp_tune 17 / 18: tile order of the fp32 batched encode / decode: 0 2-D grid (tensor =
+// blockIdx.y), 1 one flat tensor-major grid, 2 the flat grid in XCD-aware order
+std::atomic<int> g_batch_order[2] = {{0}, {0}};
 
 template <class Op, int B, int K, int NT>
 hipError_t launch_k(const typename Op::Args& a, long long nunits, hipStream_t s, int xcd = 0) {
@@ -598,10 +619,14 @@ EFL_API int efl_fxp_tune(int kind, int value) {
     if (value != 0 && value != 1) return EFL_E_INVALID_ARGUMENT;
     return g_e_first.exchange(value);
   }
+  if (kind == 17 || kind == 18) {   // batched fp32 tile order: 0 2-D, 1 flat, 2 flat XCD-aware
+    if (value < 0 || value > 2) return EFL_E_INVALID_ARGUMENT;
+    return g_batch_order[kind - 17].exchange(value);
+  }
   if (kind >= 10 && kind <= 13) {   // batched fp32: 10/11 encode block/K, 12/13 decode block/K
     const int dir = kind >= 12 ? kDec : kEnc;
     if (kind % 2 == 0) {
-      if (value != 256 && value != 512) return EFL_E_INVALID_ARGUMENT;
+      if (value != 128 && value != 256 && value != 512) return EFL_E_INVALID_ARGUMENT;
       return g_batch_block[dir].exchange(value);
     }
     if (value != 1 && value != 2 && value != 4) return EFL_E_INVALID_ARGUMENT;
@@ -718,11 +743,20 @@ namespace {
 template <class Op, int NT, int B, int K>
 hipError_t launch_batched_bk(const void* const* src, void* const* d0, void* const* d1,
                              const long long* ns, long long count, long long max_n, int flag,
-                             hipStream_t s) {
+                             hipStream_t s, int dir = -1) {
   const long long tile = (long long)B * K * Op::kElems;
   const long long gx = (max_n + tile - 1) / tile;
   if (gx == 0 || count == 0) return hipSuccess;
   if (gx > 0x7FFFFFFFll) return hipErrorInvalidValue;
+  const int order = dir >= 0 ? g_batch_order[dir].load(std::memory_order_relaxed) : 0;
+  const long long total = count * gx;
+  if (order > 0 && total < 0x7FFFFFF0ll) {
+    const long long per = order == 2 && total >= 64 ? (total + 7) / 8 : 0;
+    const long long grid = per ? 8 * per : total;
+    hipLaunchKernelGGL((k_batched_flat<Op, B, K, NT>), dim3((unsigned)grid), dim3(B), 0, s, src, d0, d1, ns, flag,
+                       gx, total, per);
+    return hipGetLastError();
+  }
   for (long long b = 0; b < count; b += kMaxGridY) {
     const long long gy = count - b < kMaxGridY ? count - b : kMaxGridY;
     hipLaunchKernelGGL((k_batched<Op, B, K, NT>), dim3((unsigned)gx, (unsigned)gy), dim3(B), 0, s,
@@ -748,10 +782,11 @@ hipError_t launch_batched_f32(int dir, const void* const* src, void* const* d0, 
   const int B = g_batch_block[dir].load(std::memory_order_relaxed);
   const int K = g_batch_k[dir].load(std::memory_order_relaxed);
 #define EFL_BK(B_, K_) \
-  if (B == B_ && K == K_) return launch_batched_bk<Op, NT, B_, K_>(src, d0, d1, ns, count, max_n, flag, s);
-  EFL_BK(256, 1) EFL_BK(256, 2) EFL_BK(256, 4) EFL_BK(512, 1) EFL_BK(512, 2) EFL_BK(512, 4)
+  if (B == B_ && K == K_) return launch_batched_bk<Op, NT, B_, K_>(src, d0, d1, ns, count, max_n, flag, s, dir);
+  EFL_BK(128, 1) EFL_BK(128, 2) EFL_BK(256, 1) EFL_BK(256, 2) EFL_BK(256, 4) EFL_BK(512, 1) EFL_BK(512, 2)
+  EFL_BK(512, 4)
 #undef EFL_BK
-  return launch_batched_bk<Op, NT, kBatchB, kBatchK>(src, d0, d1, ns, count, max_n, flag, s);
+  return launch_batched_bk<Op, NT, kBatchB, kBatchK>(src, d0, d1, ns, count, max_n, flag, s, dir);
 }
 }  // namespace
 

@@ -3,6 +3,7 @@
 Public names mirror efls-train/python/efl (exporter registry, efl/__init__.py:47):
   efl.paillier.fixedpoint.{encode, decode, Tensor}, efl.paillier.{Keypair, Tensor}
   efl.Communicator (gRPC TrainerService, pre-send/post-recv hooks), efl.privacy.FixedPointHook
+  efl.FederalModel (create_keypair, paillier_{sender,recver}_{dense,weight}, minimize), efl.MODE
   efl.secret_sharing.{matmul, Dense, dense, share, reveal}
   efl.privacy.{DPGradientDescentGaussianOptimizer, DPAdamOptimizer, ..., make_optimizer_class}
   efl.HexTensor (the DT_STRING stand-in), efl.lib.ops (the `fed_ops` namespace)
@@ -22,6 +23,10 @@ from efl.privacy.hex_tensor import HexTensor
 from efl.framework import communicator
 from efl.framework import encrypt_hook
 from efl.framework.communicator import Communicator, TensorHook
+from efl.framework import task_scope as _task_scope
+from efl.framework import model
+from efl.framework.task_scope import MODE
+from efl.framework.model import FederalModel
 
 exporter.filldict(globals())
 

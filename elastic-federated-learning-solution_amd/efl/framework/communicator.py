@@ -61,6 +61,21 @@ def _env_int(name, default):
     return int(v) if v else default
 
 
+def _http2_opts():
+    """HTTP/2 transport options for the large-message path (both server and client). Frame size:
+    the largest the protocol allows instead of 16 KiB, so a 512 MiB message is 32 frames, not
+    32 Ki (EFL_GRPC_MAX_FRAME_SIZE, 0 = gRPC's default)."""
+    frame = _env_int("EFL_GRPC_MAX_FRAME_SIZE", 0)
+    out = []
+    if frame:
+        out.append(("grpc.http2.max_frame_size", frame))
+    extra = os.environ.get("EFL_GRPC_OPTIONS", "")
+    for kv in filter(None, extra.split(",")):
+        k, v = kv.split("=", 1)
+        out.append((k, int(v)))
+    return out
+
+
 def _read(path):
     with open(path, "rb") as f:
         return f.read()
@@ -126,7 +141,7 @@ class Communicator(object):
     def __init__(self, federal_role, worker_index, worker_num, peer_addr, local_addr,
                  client_thread_num=None, server_thread_num=None,
                  scanning_interval_milliseconds=None, default_timeout_milliseconds=None,
-                 hooks=None, strict_names=False, connect_retry_seconds=10.0):
+                 hooks=None, strict_names=False, connect_retry_seconds=10.0, channels=None):
         if federal_role not in ("leader", "follower"):
             raise ValueError("federal_role must be set one of [leader/follower] in Communicator")
         self._federal_role = federal_role
@@ -139,6 +154,12 @@ class Communicator(object):
         self._hooks = list(hooks or [])
         self._strict = strict_names
         self._retry = connect_retry_seconds
+        # client connections to the peer (the reference opens one channel per peer,
+        # communicator_ops.cc:462); EFL_CHANNELS overrides. Any count speaks the same protocol.
+        # Two: a hook's mantissa and exponent messages (512 MiB each at config 5) travel on two TCP
+        # connections at once, 1.26-1.34 -> 1.44-1.45 GB/s on the MI355X box's host
+        # (tools/grpc_probe.py, profiles/r03/grpc_probe.jsonl); four was no faster.
+        self._nchan = max(1, int(channels if channels is not None else _env_int("EFL_CHANNELS", 2)))
         self._local_step = [0] * worker_num
         self._recv_set = set()
         self._lock = threading.Lock()
@@ -218,8 +239,8 @@ class Communicator(object):
                     p.finish(1, "communicator shut down")   # CANCELLED
         if self._server is not None:
             self._server.stop(grace=1.0).wait()
-        if self._channel is not None:
-            self._channel.close()
+        for ch in getattr(self, "_channels", []):
+            ch.close()
         self._status = "CLOSED"
 
     @property
@@ -249,6 +270,7 @@ class Communicator(object):
     def _start_server(self):
         opts = [("grpc.max_send_message_length", _env_int("EFL_SERVER_MAX_SEND_MESSAGE_SIZE", 1 << 30)),
                 ("grpc.max_receive_message_length", _env_int("EFL_SERVER_MAX_RECEIVE_MESSAGE_SIZE", 1 << 30))]
+        opts += _http2_opts()
         server = grpc.server(futures.ThreadPoolExecutor(max_workers=self._server_threads), options=opts)
         handlers = {
             "SendMessage": grpc.unary_unary_rpc_method_handler(self._on_send_message),
@@ -272,16 +294,25 @@ class Communicator(object):
     def _start_client(self):
         opts = [("grpc.max_send_message_length", _env_int("EFL_CLIENT_MAX_SEND_MESSAGE_SIZE", 1 << 30)),
                 ("grpc.max_receive_message_length", _env_int("EFL_CLIENT_MAX_RECEIVE_MESSAGE_SIZE", 1 << 30))]
+        opts += _http2_opts()
         override = os.environ.get("EFL_SSL_TARGET_NAME_OVERRIDE", "")
         if override:
             opts.append(("grpc.ssl_target_name_override", override))
         peer_certs = os.environ.get("EFL_PEER_CERTS_FILENAME", "")
-        if peer_certs:
-            self._channel = grpc.secure_channel(
-                self._peer_addr, grpc.ssl_channel_credentials(root_certificates=_read(peer_certs)), opts)
-        else:
-            self._channel = grpc.insecure_channel(self._peer_addr, opts)
-        self._send_rpc = self._channel.unary_unary(_SEND)
+
+        def channel(k):
+            # a local subchannel pool per channel: each is its own TCP connection (channels with
+            # equal arguments would otherwise share one connection through the global pool)
+            o = opts + ([("grpc.use_local_subchannel_pool", 1), ("efl.channel_index", k)] if self._nchan > 1 else [])
+            if peer_certs:
+                return grpc.secure_channel(
+                    self._peer_addr, grpc.ssl_channel_credentials(root_certificates=_read(peer_certs)), o)
+            return grpc.insecure_channel(self._peer_addr, o)
+        self._channels = [channel(k) for k in range(self._nchan)]
+        self._channel = self._channels[0]
+        self._send_rpcs = [ch.unary_unary(_SEND) for ch in self._channels]
+        self._send_rpc = self._send_rpcs[0]
+        self._next_chan = 0
 
     # server side ---------------------------------------------------------------------
     def _on_connect(self, request, context):
@@ -333,7 +364,12 @@ class Communicator(object):
             shape = tuple(t.shape)
             content = t.view(torch.uint8).numpy().reshape(-1) if t.numel() else b""
         req = wire.message_request(name, self.step, dtype, shape, content)
-        fut = self._send_rpc.future(req, timeout=self._timeout)
+        # messages round-robin over the channels: two large payloads sent back to back (a hook's
+        # mantissa and exponent) travel on two connections at once
+        with self._lock:
+            rpc = self._send_rpcs[self._next_chan]
+            self._next_chan = (self._next_chan + 1) % len(self._send_rpcs)
+        fut = rpc.future(req, timeout=self._timeout)
         return SendHandle([(name, fut)])
 
     def _take(self, name, step):

@@ -356,6 +356,7 @@ class KeyBlock:
         self.block, self.ptr = head, head.data_ptr()
         src = reuse_table
         if src is not None and (src.n, src.hs, src.a_bits, src.table_window, src.lc) == (n, hs, a_bits, W, self.lc) \
+                and torch.device(src.device) == torch.device(self.device) \
                 and (src.desc.off_table28 >= 0) == bool(L28) and (not L28 or src.desc.n2_28_len == L28):
             # set_private_key on a key whose public part is unchanged: the tables are the same
             o32, o28 = src.desc.off_table, src.desc.off_table28

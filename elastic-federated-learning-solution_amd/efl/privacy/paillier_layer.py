@@ -281,11 +281,20 @@ def cached_layers(communicator) -> dict:
     return reg
 
 
-def _cached(communicator, key, build):
+def _cached(communicator, key, build, keypair=None, units=None):
+    """The layer built for `key` on this communicator (built on first use). A later call with a
+    different keypair object (a rotated key) re-points the layer at it; one with a different
+    `units` is an error, as TF's variable reuse with a mismatched shape is."""
     reg = cached_layers(communicator)
     layer = reg.get(key)
     if layer is None:
         layer = reg[key] = build()
+        return layer
+    if units is not None and getattr(layer, "units", units) != units:
+        from efl import errors
+        raise errors.InvalidArgumentError(f"layer {key} was built with units={layer.units}, called with {units}")
+    if keypair is not None and getattr(layer, "keypair", keypair) is not keypair:
+        layer.keypair = keypair
     return layer
 
 
@@ -313,7 +322,7 @@ def _plain_dense(in_features, units, use_bias, kernel_initializer, bias_initiali
 def dense_send(inputs, keypair, communicator, prefix, units, name=None, reuse=None, seed=None):
     layer = _cached(communicator, ("sender.dense", prefix, name),
                     lambda: PaillierActiveDense(keypair, communicator, prefix, units, name=name, _reuse=reuse,
-                                                seed=seed))
+                                                seed=seed), keypair, units)
     return layer(inputs), layer.kernel
 
 
@@ -322,7 +331,7 @@ def dense_recv(inputs, keypair, communicator, prefix, recv_shape, units, activat
                kernel_initializer=None, bias_initializer=None, name=None, reuse=None, seed=None, **_unused):
     layer = _cached(communicator, ("recver.dense", prefix, name),
                     lambda: PaillierPassiveDense(keypair, communicator, prefix, units,
-                                                 kernel_initializer=kernel_initializer, seed=seed))
+                                                 kernel_initializer=kernel_initializer, seed=seed), keypair, units)
     x_exponent = communicator.recv(prefix + "_[x]_exponent", shape=recv_shape, dtype=torch.int64)
     y = layer(x_exponent.to(_device_of(inputs)))
     if inputs is not None:
@@ -338,7 +347,7 @@ def dense_recv(inputs, keypair, communicator, prefix, recv_shape, units, activat
 @exporter.export("paillier.sender.weight")
 def weight_send(inputs, keypair, communicator, prefix, units, seed=None):
     layer = _cached(communicator, ("sender.weight", prefix, None),
-                    lambda: PaillierActiveWeight(keypair, communicator, prefix, units, seed=seed))
+                    lambda: PaillierActiveWeight(keypair, communicator, prefix, units, seed=seed), keypair, units)
     return layer(inputs), layer.kernel
 
 
@@ -346,7 +355,7 @@ def weight_send(inputs, keypair, communicator, prefix, units, seed=None):
 def weight_recv(inputs, keypair, communicator, prefix, units, kernel_initializer=None, seed=None):
     layer = _cached(communicator, ("recver.weight", prefix, None),
                     lambda: PaillierPassiveWeight(keypair, communicator, prefix, units,
-                                                  kernel_initializer=kernel_initializer, seed=seed))
+                                                  kernel_initializer=kernel_initializer, seed=seed), keypair, units)
     x_exponent = communicator.recv(prefix + "_[x]_exponent", shape=(-1, units), dtype=torch.int64)
     y = layer(x_exponent.to(_device_of(inputs)))
     if inputs is not None:

@@ -11,7 +11,8 @@
  * Conventions
  *  - Every payload pointer is DEVICE memory owned by the caller; the library never synchronises:
  *    work is enqueued on `stream` (NULL = default stream). It allocates nothing except the
- *    stream-ordered scratch of efl_pl_matmul and of the sliced efl_pl_decrypt (see there).
+ *    stream-ordered scratch of efl_pl_matmul, of the sliced efl_pl_decrypt and of efl_pl_fxp_add
+ *    in the kernel families without its fused kernel (see there).
  *  - Return value: 0 on success, otherwise the NEGATED TensorFlow error code
  *    (tensorflow/core/lib/core/error_codes.proto; the reference reports errors as TF Status):
  *      -3 INVALID_ARGUMENT, -8 RESOURCE_EXHAUSTED, -9 FAILED_PRECONDITION, -10 ABORTED,
@@ -72,7 +73,9 @@ const char* efl_last_error(void);
  * kinds 10 / 11 = workgroup size (256, 512) / pairs per lane (1, 2, 4) of the fp32 batched encode,
  * 12 / 13 the same for the batched decode; kinds 14 / 15 = XCD-aware tile order (0 / 1; each of the
  * 8 XCDs streams one contiguous eighth) of the fp32 streaming encode / decode (default 0 / 1);
- * kind 16 = the streaming fp32 encode stores the exponent pair before the mantissa pair (0 / 1).
+ * kind 16 = the streaming fp32 encode stores the exponent pair before the mantissa pair (0 / 1);
+ * kinds 17 / 18 = tile order of the fp32 batched encode / decode (0 2-D grid, 1 one flat tensor-major
+ * grid, 2 the flat grid in XCD-aware order); batched workgroup sizes 128, 256, 512.
  * Returns the previous value or EFL_E_INVALID_ARGUMENT. */
 int efl_fxp_tune(int kind, int value);
 

@@ -1,0 +1,144 @@
+"""GPU: efl.FederalModel's Paillier entry points (efls-train/python/efl/framework/model.py:543-677)
+and their learning-rate update of the Paillier kernels (model.py:808-814) over three training steps
+of two parties, each its own process, on loopback.
+
+What is checked (in the parent, against float64 arithmetic of the same protocol):
+  * step by step, W_recv + w_send moves by exactly -lr * x^T q(dy): the receiver applies
+    lr * (dw + nf), the sender lr * (-nf) with the PEER's rate, and the masks cancel
+    (q = the reference's decrease_precision fixed-point rounding of dy, paillier_layer.py:123);
+  * each forward output equals x @ q(W_recv) + x @ w_send (the encrypted product with the
+    receiver's kernel rounded the same way, plus the sender's local share), and the sender's own
+    copy of it is masked by the receiver's noise n1;
+  * W_recv + w_send tracks plaintext SGD of 0.5 |x W - t|^2 from the same start;
+  * neither share alone is the model: the sender's share is non-zero and masked.
+Dense and Weight layers both."""
+import multiprocessing as mp
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import fxp
+from test_communicator import free_port
+
+pytestmark = pytest.mark.gpu
+
+B, F, STEPS, LR = 16, 6, 3, 0.05
+
+
+def data(kind):
+    g = torch.Generator().manual_seed(11)
+    units = 4 if kind == "dense" else F
+    xs = [torch.randn(B, F, generator=g) for _ in range(STEPS)]
+    t = torch.randn(B, units, generator=g)
+    return units, xs, t
+
+
+def party(role, kind, my, peer, q):
+    try:
+        import efl
+        Role = efl.privacy.Role
+        units, xs, t = data(kind)
+        c = efl.Communicator(role, 0, 1, f"127.0.0.1:{peer}", f"127.0.0.1:{my}",
+                             default_timeout_milliseconds=120000, connect_retry_seconds=0.1)
+        model = efl.FederalModel(c)
+        sender = role == "follower"
+        model.create_keypair("kp", Role.SENDER if sender else Role.RECEIVER, n_bytes=64, seed=7)
+        model.initialize()
+        rec = []
+        for step in range(STEPS):
+            model.begin_step()
+            if sender:
+                if kind == "dense":
+                    out = model.paillier_sender_dense(xs[step].cuda(), "kp", "l1", LR, units, seed=1)
+                else:
+                    out = model.paillier_sender_weight(xs[step].cuda(), "kp", "l1", LR, units, seed=1)
+                (w, lr), = model.paillier_vars_and_lrs()
+                before = w.detach().clone()
+                model.minimize(None)                      # no loss of its own: the outputs pull dx
+                rec.append((before, w.detach().clone(), out.detach()))
+            else:
+                if kind == "dense":
+                    y = model.paillier_recver_dense(None, "kp", "l1", LR, units, (B, F), seed=2)
+                else:
+                    gw = torch.Generator().manual_seed(3)
+                    y = model.paillier_recver_weight(None, "kp", "l1", LR, units, seed=2,
+                                                     kernel_initializer=lambda v: v.copy_(torch.rand(v.shape, generator=gw) - 0.5))
+                (W, lr), = model.paillier_vars_and_lrs()
+                before = W.detach().clone()
+                loss = 0.5 * ((y - t.cuda()) ** 2).sum()
+                dy = (y - t.cuda()).detach()
+                model.minimize(None, loss)
+                assert W.grad is None
+                rec.append((before, W.detach().clone(), y.detach(), dy))
+            model.end_step()
+        assert len(model.paillier_vars_and_lrs()) == 1          # registered once, not once per step
+        c.shutdown()
+        q.put((role, [tuple(a.cpu().numpy() for a in r) for r in rec], None))
+    except BaseException as e:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((role, None, traceback.format_exc()[-3000:]))
+
+
+def run_parties(kind):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pl, pf = free_port(), free_port()
+    procs = [ctx.Process(target=party, args=("leader", kind, pl, pf, q)),
+             ctx.Process(target=party, args=("follower", kind, pf, pl, q))]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in procs:
+            role, res, err = q.get(timeout=400)
+            assert err is None, (role, err)
+            results[role] = res
+    finally:
+        for p in procs:
+            p.join(30)
+            if p.is_alive():
+                p.kill()
+    return results
+
+
+def qdp(v):
+    """decode(encode(v, decrease_precision=True)): the rounding the protocol applies to W and dy."""
+    M, E = fxp.encode(np.ascontiguousarray(v, np.float32), decrease_precision=True)
+    return fxp.decode(M, E).astype(np.float64)
+
+
+@pytest.mark.parametrize("kind", ["dense", "weight"])
+def test_federal_model_trains_the_shared_kernel(kind):
+    res = run_parties(kind)
+    units, xs, t = data(kind)
+    t = t.numpy().astype(np.float64)
+    recv, send = res["leader"], res["follower"]
+    W_plain = recv[0][0].astype(np.float64) + send[0][0].astype(np.float64)
+    for step in range(STEPS):
+        W0, W1, y, dy = (a.astype(np.float64) for a in recv[step])
+        w0, w1, out = (a.astype(np.float64) for a in send[step])
+        x = xs[step].numpy().astype(np.float64)
+        if kind == "dense":
+            want_y = x @ qdp(W0) + x @ w0
+            grad = x.T @ qdp(dy)
+            plain_grad = x.T @ (x @ W_plain - t)
+        else:
+            want_y = x * qdp(W0) + x * w0
+            grad = (x * qdp(dy)).sum(0)
+            plain_grad = (x * (x * W_plain - t)).sum(0)
+        assert np.allclose(y, want_y, rtol=1e-4, atol=1e-4), step          # receiver's output
+        # the sender only ever sees z + n1 (paillier_layer.py:74-76): the receiver's noise masks it
+        assert np.abs(out - want_y).mean() > 0.2, step
+        # the masks cancel: the SUM of the two updates is -lr * x^T q(dy)
+        assert np.allclose((W1 + w1) - (W0 + w0), -LR * grad, rtol=1e-4, atol=2e-5), step
+        # each share moved by much more than the gradient alone (it carries the mask nf ~ N(10 s, 1))
+        assert np.abs(w1 - w0).mean() > 0.1 * LR, step
+        W_plain = W_plain - LR * plain_grad
+        # the model the two parties hold together follows plaintext SGD (fixed-point rounding of
+        # the encrypted product and of dy only)
+        assert np.allclose(W1 + w1, W_plain, rtol=2e-2, atol=2e-3), step
+        if step + 1 < STEPS:                       # next step starts from this step's result
+            assert np.array_equal(recv[step + 1][0], recv[step][1])
+            assert np.array_equal(send[step + 1][0], send[step][1])
+    assert np.abs(send[-1][1]).mean() > 0.1 * LR              # the sender's share is not zero

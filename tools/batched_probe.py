@@ -16,6 +16,8 @@ import efl  # noqa: E402
 
 ARMS = {"256x4": (256, 4, 256, 4), "256x2": (256, 2, 256, 2), "256x1": (256, 1, 256, 1),
         "512x4": (512, 4, 512, 4), "512x2": (512, 2, 512, 2), "512x1": (512, 1, 512, 1)}
+# arm = (enc block, enc K, dec block, dec K[, enc order, dec order]); order (efl_fxp_tune 17 / 18):
+# 0 2-D grid, 1 flat, 2 flat XCD-aware
 if os.environ.get("BATCH_ARMS"):
     ARMS = {a.split(":")[0]: tuple(int(v) for v in a.split(":")[1].split(",")) for a in os.environ["BATCH_ARMS"].split(";")}
 dev = efl.lib.require_gpu()
@@ -37,8 +39,10 @@ def step():
 
 res = {a: [] for a in ARMS}
 for r in range(9):
-    for a, (eb, ek, db, dk) in ARMS.items():
-        for kind, v in ((10, eb), (11, ek), (12, db), (13, dk)):
+    for a, arm in ARMS.items():
+        eb, ek, db, dk = arm[:4]
+        oe, od = arm[4:6] if len(arm) >= 6 else (0, 0)
+        for kind, v in ((10, eb), (11, ek), (12, db), (13, dk), (17, oe), (18, od)):
             efl.lib.check(min(0, lib.efl_fxp_tune(kind, v)))
         for _ in range(3):
             step()
