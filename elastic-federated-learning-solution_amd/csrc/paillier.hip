@@ -953,14 +953,18 @@ inline int ln_index(int ln) { return ln == 16 ? 0 : ln == 32 ? 1 : ln == 64 ? 2 
 inline int slicing(int ln, int dec) { return g_slicing[ln_index(ln)][dec]; }
 bool g_slicing_set[4][2] = {};   // set explicitly through efl_pl_tune: used as given for every size
 
-// Decryption family for n elements: the default (measured at >= 100k elements) unless the launch
-// would leave SIMDs without a wave; then more lanes per element (profiles/r01/sweep_small_n.jsonl:
-// 32k decrypts at 1024-bit, 2.57 M/s with 32 limbs per lane, 3.29 M/s with 16)
+// Decryption family for n elements: the default (C = 32) unless the launch would give fewer than
+// 768 waves (3 per 4 SIMDs) of that family; then C = 8 (four times the lanes per element). Round 3
+// sweep of the current kernels (tools/sweep_dec_family.py, profiles/r03/dec_family.jsonl): 1024-bit
+// n at 32,768 elements 7.9 ms with C = 8, 8.1 with 16, 10.4 with 32, and at 50,176 C = 32 wins
+// (10.5 against 11.9 / 13.2); 2048-bit 16,384: 31.7 (C = 8) against 37.2 (32); 4096-bit 4,096: 90
+// against 143. C = 16 is never the fastest (at 2048 / 4096 bits it spills into its window loop and
+// runs 3-5x slower), so the sizing skips it; round 1's rule halved C step by step.
 inline int decrypt_family(int ln, long long n) {
-  int C = slicing(ln, 1);
+  const int C = slicing(ln, 1);
   if (!C || g_slicing_set[ln_index(ln)][1]) return C;
-  constexpr long long kOneWavePerSimd = 256ll * 4 * 64;
-  while (C > 8 && n * (ln / C) < kOneWavePerSimd && pl::sliced_available(ln, C / 2)) C /= 2;
+  constexpr long long kFewWaves = 768ll * 64;   // lanes of 768 waves
+  if (C == 32 && n * (ln / 32) < kFewWaves && pl::sliced_available(ln, 8)) return 8;
   return C;
 }
 

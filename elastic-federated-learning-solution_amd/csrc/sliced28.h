@@ -99,7 +99,9 @@ template <int C, int G, class B>
 __device__ __forceinline__ void mont_mul(uint32_t (&a)[C], const B& b, const uint32_t (&m)[C], uint32_t minv,
                                          int g) {
   constexpr int L = C * G;
-  constexpr int kUnroll = G == 1 ? 1 : EFL_MONT28_UNROLL;
+  // one step per pass for one-lane numbers and for short slices (C < 32: the 128-VGPR decryption
+  // families C = 8 / 16, where two steps per pass spilled 736-1,092 VGPRs into the loop)
+  constexpr int kUnroll = (G == 1 || C < 32) ? 1 : EFL_MONT28_UNROLL;
   uint64_t T[C];
 #pragma unroll
   for (int j = 0; j < C; ++j) T[j] = 0;

@@ -18,10 +18,13 @@ Box-Muller) from a per-process `NoiseStream`. The per-microbatch gradients are a
 clip is a torch reduction. No CPU fallback: the kernel needs the GPU.
 
 Torch mapping. TF optimisers get their variables at minimize time; torch ones at construction.
-These classes take either: `params` as the torch optimiser does, or none (the reference's call
-shape, e.g. `DPGradientDescentGaussianOptimizer(noise_multiplier=1.0, learning_rate=0.25)`), in
-which case the wrapped optimiser is built on the first `compute_gradients` / `minimize` var_list.
-`learning_rate` is accepted for `lr`.
+These classes take either: `params` (as `params=`, or first positional with the DP arguments as
+keywords, torch style: `DPAdamGaussianOptimizer(model.parameters(), noise_multiplier=1.0, lr=..)`),
+or none (the reference's call shape, e.g. `DPGradientDescentGaussianOptimizer(noise_multiplier=1.0,
+learning_rate=0.25)`), in which case the wrapped optimiser is built on the first
+`compute_gradients` / `minimize` var_list. `learning_rate` is accepted for `lr`. Float64 (and
+half-precision) variables train: their noise is TF's float32 normal cast to the variable's dtype,
+and the clip norm is taken in float64 for float64 records.
 
 One reference quirk is kept: each microbatch's loss is `reduce_func(tf.gather(loss, [i]), axis=0)`
 (:172), a reduction over a length-1 axis, so 'mean' and 'sum' both leave the row as it is and its
@@ -51,8 +54,13 @@ def dp_noise(x: torch.Tensor, mode: int, sigma: float, divisor: float = 1.0, str
     """efl_dp_noise over one float32 tensor: mode 0 (x + z x sigma) / divisor, mode 1
     (x + z sigma) / divisor, z ~ N(0, 1) drawn from `stream` (default: the process's)."""
     x = lib.as_tensor(x)
+    if not x.dtype.is_floating_point:
+        raise errors.InvalidArgumentError(f"DP noise needs a floating-point gradient, got {x.dtype}")
     if x.dtype != torch.float32:
-        raise errors.InvalidArgumentError(f"DP noise is float32 (tf.random.normal's default), got {x.dtype}")
+        # the reference draws tf.random.normal(..., dtype=v.dtype); the kernel draws TF's float32
+        # normal, so other float dtypes are noised in float32 and cast back (float64 variables keep
+        # float32-accurate noise; parity with TF's noise stream is distributional either way)
+        return dp_noise(x.float(), mode, sigma, divisor, stream).to(x.dtype)
     v, home = lib.on_device(x.detach())
     v = v.contiguous()
     if v.data_ptr() % 16:
@@ -104,9 +112,11 @@ class GaussianSumQuery(_SumQuery):
         return self._l2_norm_clip
 
     def preprocess_record(self, params, record):
-        # tf.clip_by_global_norm: t * clip * min(1 / ||record||, 1 / clip)
-        norm = torch.sqrt(sum((t.float() * t.float()).sum() for t in record))
-        scale = params * torch.minimum(1.0 / norm, torch.tensor(1.0 / params, device=norm.device))
+        # tf.clip_by_global_norm: t * clip * min(1 / ||record||, 1 / clip), in the record's dtype
+        # (the widest of its tensors)
+        dt = torch.float64 if any(t.dtype == torch.float64 for t in record) else torch.float32
+        norm = torch.sqrt(sum((t.to(dt) * t.to(dt)).sum() for t in record))
+        scale = params * torch.minimum(1.0 / norm, torch.tensor(1.0 / params, dtype=dt, device=norm.device))
         return [t * scale.to(t.dtype) for t in record]
 
     def get_noised_result(self, sample_state, global_state, divisor: float = 1.0):
@@ -136,14 +146,58 @@ def _split_params(args, kwargs):
     return None, args
 
 
+def _bind(args, kwargs, *spec):
+    """Bind the leading (name, default) parameters from positional args, then keywords; returns
+    their values followed by the remaining positional args."""
+    args = list(args)
+    vals = []
+    for name, default in spec:
+        if args:
+            if name in kwargs:
+                raise TypeError(f"got multiple values for argument {name!r}")
+            vals.append(args.pop(0))
+        else:
+            vals.append(kwargs.pop(name, default))
+    return (*vals, tuple(args))
+
+
+def _as_params(obj):
+    """obj as a torch optimiser's params (a list of tensors or param-group dicts), or None when it
+    is something else (a number, a query): lets `DPAdamGaussianOptimizer(model.parameters(), lr=..)`
+    work although the reference's first positional argument is noise_multiplier."""
+    if obj is None or isinstance(obj, (int, float, bool, str)) or hasattr(obj, "get_noised_result"):
+        return None
+    if isinstance(obj, torch.Tensor):
+        return [obj]
+    try:
+        items = list(obj)
+    except TypeError:
+        return None
+    if items and all(isinstance(t, (torch.Tensor, dict)) for t in items):
+        return items
+    return None
+
+
 @exporter.export("privacy.make_optimizer_class")
 def make_optimizer_class(cls):
     """A DP subclass of the torch optimiser class `cls` (dp_optimizer.py:80-220)."""
 
     class DPOptimizerClass(cls):
-        def __init__(self, dp_sum_query, num_microbatches=None, unroll_microbatches=False, *args, **kwargs):
+        def __init__(self, *args, **kwargs):
+            """(dp_sum_query, num_microbatches=None, unroll_microbatches=False, [params], **opt
+            kwargs), or torch style (params, dp_sum_query=..., ...)."""
             if "learning_rate" in kwargs:
                 kwargs["lr"] = kwargs.pop("learning_rate")
+            lead = _as_params(args[0]) if args else None
+            if lead is not None:    # params first, torch style: the DP arguments are keywords then
+                if "dp_sum_query" not in kwargs:
+                    raise TypeError("params given first: pass dp_sum_query= as a keyword")
+                kwargs["params"] = lead
+                args = args[1:]
+            dp_sum_query, num_microbatches, unroll_microbatches, args = _bind(
+                args, kwargs, ("dp_sum_query", None), ("num_microbatches", None), ("unroll_microbatches", False))
+            if dp_sum_query is None:
+                raise TypeError("dp_sum_query is required")
             params, args = _split_params(args, kwargs)
             self._dp_sum_query = dp_sum_query
             self._num_microbatches = num_microbatches
@@ -214,8 +268,16 @@ def make_gaussian_optimizer_class(cls):
     each summed gradient without l2_norm_clip, clipped records + N(0, (clip * mult)^2) with it."""
 
     class DPGaussianOptimizerClass(make_optimizer_class(cls)):
-        def __init__(self, noise_multiplier=0, l2_norm_clip=None, num_microbatches=None, unroll_microbatches=False,
-                     *args, **kwargs):
+        def __init__(self, *args, **kwargs):
+            """(noise_multiplier=0, l2_norm_clip=None, num_microbatches=None,
+            unroll_microbatches=False, [params], **opt kwargs), or torch style (params, ...)."""
+            lead = _as_params(args[0]) if args else None
+            if lead is not None:    # torch style: params first, the DP arguments as keywords
+                kwargs["params"] = lead
+                args = args[1:]
+            noise_multiplier, l2_norm_clip, num_microbatches, unroll_microbatches, args = _bind(
+                args, kwargs, ("noise_multiplier", 0), ("l2_norm_clip", None), ("num_microbatches", None),
+                ("unroll_microbatches", False))
             if l2_norm_clip is None:
                 q = ElementWiseGaussianSumQuery(noise_multiplier)
             else:

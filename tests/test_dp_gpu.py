@@ -135,3 +135,20 @@ def test_optimizer_step_matches_oracle(dp, clip):
         ctr += (n + 3) // 4
         want = v0.cpu().numpy().reshape(-1) - 0.5 * g
         assert np.allclose(v.detach().cpu().numpy().reshape(-1), want, rtol=1e-4, atol=1e-5)
+
+
+def test_float64_and_half_gradients_take_the_float32_noise(dp):
+    """float64 (and bf16) gradients are noised, not rejected: the kernel's float32 noise
+    of the float32 value, cast back to the gradient's dtype (same stream position, same bits)."""
+    from efl.privacy.secret_sharing import NoiseStream
+    x = torch.randn(1001, dtype=torch.float64, generator=torch.Generator().manual_seed(3)).cuda()
+    got = dp.dp_noise(x, 0, 0.9, 4.0, NoiseStream(12, 5))
+    assert got.dtype == torch.float64
+    want = dp.dp_noise(x.float(), 0, 0.9, 4.0, NoiseStream(12, 5)).double()
+    assert torch.equal(got, want)
+    xb = x.to(torch.bfloat16)
+    gb = dp.dp_noise(xb, 1, 1.0, 1.0, NoiseStream(12, 5))
+    assert gb.dtype == torch.bfloat16
+    assert torch.equal(gb, dp.dp_noise(xb.float(), 1, 1.0, 1.0, NoiseStream(12, 5)).to(torch.bfloat16))
+    with pytest.raises(Exception, match="floating-point"):
+        dp.dp_noise(torch.ones(4, dtype=torch.int32, device="cuda"), 0, 1.0, 1.0, NoiseStream(1, 0))

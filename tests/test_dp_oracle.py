@@ -107,3 +107,33 @@ def test_deferred_params_and_learning_rate_alias():
     assert opt._built and opt.param_groups[0]["lr"] == 0.25
     # mean over 2 microbatches of d/dw (w - t)^2 = -2 t: (-2 - 6) / 2, (-4 - 8) / 2; w -= 0.25 g
     assert torch.allclose(w.detach(), torch.tensor([1.0, 1.5]))
+
+
+def test_params_first_torch_style_and_float64():
+    """`DPAdamGaussianOptimizer(model.parameters(), noise_multiplier=.., lr=..)` binds the
+    parameters (not noise_multiplier); float64 variables train with a float64 clip norm."""
+    import efl
+    lin = torch.nn.Linear(3, 2).double()
+    opt = efl.privacy.DPAdamGaussianOptimizer(lin.parameters(), noise_multiplier=0.7, l2_norm_clip=1.5, lr=0.01)
+    assert opt._built and len(opt.param_groups[0]["params"]) == 2
+    assert opt._dp_sum_query._stddev == pytest.approx(1.5 * 0.7)
+    opt2 = efl.privacy.DPGradientDescentGaussianOptimizer(params=list(lin.parameters()), noise_multiplier=1.0, lr=0.1)
+    assert opt2._built
+    q = efl.privacy.make_optimizer_class(torch.optim.SGD)(list(lin.parameters()), dp_sum_query=NoNoise(0.5), lr=0.1)
+    assert q._built and isinstance(q._dp_sum_query, NoNoise)
+    with pytest.raises(TypeError, match="dp_sum_query"):
+        efl.privacy.make_optimizer_class(torch.optim.SGD)(list(lin.parameters()), lr=0.1)
+    # float64 records: clip in float64, gradients stay float64
+    x = torch.randn(4, 3, dtype=torch.float64, generator=torch.Generator().manual_seed(1))
+    opt3 = efl.privacy.make_optimizer_class(torch.optim.SGD)(NoNoise(0.5), 4, False, list(lin.parameters()), lr=0.1)
+    got = opt3.compute_gradients((lin(x) ** 2).sum(dim=1), list(lin.parameters()))
+    assert all(g.dtype == torch.float64 for g, _ in got)
+    rows = [torch.autograd.grad((lin(x[i:i + 1]) ** 2).sum(), list(lin.parameters())) for i in range(4)]
+    want = [torch.zeros_like(p) for p in lin.parameters()]
+    for gr in rows:
+        norm = torch.sqrt(sum((g * g).sum() for g in gr))
+        s = 0.5 * min(1 / float(norm), 1 / 0.5)
+        for w, g in zip(want, gr):
+            w += g * s
+    for (g, _), w in zip(got, want):
+        assert torch.allclose(g, w / 4, rtol=1e-12, atol=1e-14)
