@@ -655,10 +655,15 @@ def main():
     dominant = "encode" if t_enc >= t_dec else "decode"
     t_dom = max(t_enc, t_dec) * 1e-3
     achieved = BYTES_PER_ELEM_KERNEL * n / t_dom / 1e9
-    traffic = None
+    traffic, traffic_source = None, None
     tr = load_traffic()
     if tr and tr.get("elements") == n and dominant in tr.get("kernels", {}):
         traffic = tr["kernels"][dominant].get("hbm_bytes_per_launch")
+        # a recorded measurement, not one of this run: say which
+        traffic_source = ("profiles/pmc_traffic.json (not measured in this run): " +
+                          tr.get("command", "rocprofv3 FETCH_SIZE / WRITE_SIZE passes of bench.py") +
+                          (f"; {tr['profile_dir']}" if tr.get("profile_dir") else "") +
+                          (f"; library {tr['library']}" if tr.get("library") else ""))
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -679,7 +684,7 @@ def main():
                                   f"seed broadcast"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
                      "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
-                     "traffic": traffic, "kernel": dominant,
+                     "traffic": traffic, "traffic_source": traffic_source, "kernel": dominant,
                      "algorithmic_bytes_per_launch": BYTES_PER_ELEM_KERNEL * n,
                      "timing": "HIP events around each launch, second pass of K steps after the timed region"},
         "kernels_ms": {"encode": round(t_enc, 4), "decode": round(t_dec, 4)},

@@ -411,6 +411,71 @@ __global__ __launch_bounds__(B) void k_batched_flat(const void* const* src, void
   batched_tile<Op, B, K, NT>(src, dst0, dst1, ns, flag, lin / gx, lin % gx);
 }
 
+// Persistent batched walk: gridDim.x workgroups over the count x gx tiles (tensor-major), workgroup
+// b taking tiles b, b + grid, ... The NEXT tile's pointer-table entries and data loads are issued
+// before the current tile's transform and stores (software pipelining), so a tile exposes neither
+// the table latency nor its data latency. Full, aligned tiles take that path; the others (ragged
+// ends, unaligned tensors) go through batched_tile.
+template <class Op, int B, int K>
+__device__ __forceinline__ bool persist_setup(const void* const* src, void* const* dst0, void* const* dst1,
+                                              const long long* ns, int flag, long long lin, long long gx,
+                                              typename Op::Args& a, long long& u0) {
+  const long long t = lin / gx, x = lin % gx;
+  const long long n = ns[t];
+  if constexpr (std::is_same<typename Op::Args, EncArgs>::value) {
+    a = EncArgs{src[t], (long long*)dst0[t], (long long*)dst1[t], flag};
+  } else {
+    a = DecArgs{(const long long*)src[t], (const long long*)dst0[t], dst1[t], flag};
+  }
+  u0 = x * B * K;
+  return aligned(src[t], 16) && aligned(dst0[t], 16) && aligned(dst1[t], 16) &&
+         u0 + (long long)B * K <= n / Op::kElems;
+}
+
+template <class Op, int B, int K, int NT>
+__global__ __launch_bounds__(B) void k_batched_persist(const void* const* src, void* const* dst0,
+                                                       void* const* dst1, const long long* ns, int flag,
+                                                       long long gx, long long total) {
+  long long lin = blockIdx.x;
+  if (lin >= total) return;
+  typename Op::Args a;
+  long long u0;
+  bool fast = persist_setup<Op, B, K>(src, dst0, dst1, ns, flag, lin, gx, a, u0);
+  typename Op::In v[K];
+  if (fast) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = Op::template load<NT>(a, u0 + k * B + threadIdx.x);
+  }
+  for (;;) {
+    const long long nxt = lin + gridDim.x;
+    typename Op::Args an;
+    long long un = 0;
+    bool fn = false;
+    typename Op::In vn[K];
+    if (nxt < total) {
+      fn = persist_setup<Op, B, K>(src, dst0, dst1, ns, flag, nxt, gx, an, un);
+      if (fn) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) vn[k] = Op::template load<NT>(an, un + k * B + threadIdx.x);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (fast) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) Op::template apply<NT>(a, u0 + k * B + threadIdx.x, v[k]);
+    } else {
+      batched_tile<Op, B, K, NT>(src, dst0, dst1, ns, flag, lin / gx, lin % gx);
+    }
+    if (nxt >= total) break;
+    lin = nxt;
+    a = an;
+    u0 = un;
+    fast = fn;
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = vn[k];
+  }
+}
+
 // Hex mantissa decode (FixedPointToFloatPointOp<string, T>, fixed_point.cc:255-257): one lane per
 // string; keeps the leading 64 bits of |m| and its bit length (mpf truncation composes to that).
 template <bool F64>
@@ -497,6 +562,8 @@ std::atomic<int> g_batch_k[2] = {{2}, {kBatchK}};
 // efl_fxp_tune 17 / 18: tile order of the fp32 batched encode / decode: 0 2-D grid (tensor =
 // blockIdx.y), 1 one flat tensor-major grid, 2 the flat grid in XCD-aware order
 std::atomic<int> g_batch_order[2] = {{0}, {0}};
+// efl_fxp_tune 19: workgroups of the persistent batched walk (order 3)
+std::atomic<int> g_batch_persist_grid{2048};
 
 template <class Op, int B, int K, int NT>
 hipError_t launch_k(const typename Op::Args& a, long long nunits, hipStream_t s, int xcd = 0) {
@@ -619,8 +686,12 @@ EFL_API int efl_fxp_tune(int kind, int value) {
     if (value != 0 && value != 1) return EFL_E_INVALID_ARGUMENT;
     return g_e_first.exchange(value);
   }
-  if (kind == 17 || kind == 18) {   // batched fp32 tile order: 0 2-D, 1 flat, 2 flat XCD-aware
-    if (value < 0 || value > 2) return EFL_E_INVALID_ARGUMENT;
+  if (kind == 19) {                 // persistent batched walk: workgroups
+    if (value < 1) return EFL_E_INVALID_ARGUMENT;
+    return g_batch_persist_grid.exchange(value);
+  }
+  if (kind == 17 || kind == 18) {   // batched fp32 tile order: 0 2-D, 1 flat, 2 flat XCD-aware, 3 persistent
+    if (value < 0 || value > 3) return EFL_E_INVALID_ARGUMENT;
     return g_batch_order[kind - 17].exchange(value);
   }
   if (kind >= 10 && kind <= 13) {   // batched fp32: 10/11 encode block/K, 12/13 decode block/K
@@ -750,6 +821,13 @@ hipError_t launch_batched_bk(const void* const* src, void* const* d0, void* cons
   if (gx > 0x7FFFFFFFll) return hipErrorInvalidValue;
   const int order = dir >= 0 ? g_batch_order[dir].load(std::memory_order_relaxed) : 0;
   const long long total = count * gx;
+  if (order == 3 && total < 0x7FFFFFF0ll) {
+    const long long cap = g_batch_persist_grid.load(std::memory_order_relaxed);
+    const long long grid = total < cap ? total : cap;
+    hipLaunchKernelGGL((k_batched_persist<Op, B, K, NT>), dim3((unsigned)grid), dim3(B), 0, s, src, d0, d1, ns, flag,
+                       gx, total);
+    return hipGetLastError();
+  }
   if (order > 0 && total < 0x7FFFFFF0ll) {
     const long long per = order == 2 && total >= 64 ? (total + 7) / 8 : 0;
     const long long grid = per ? 8 * per : total;

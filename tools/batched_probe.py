@@ -17,7 +17,7 @@ import efl  # noqa: E402
 ARMS = {"256x4": (256, 4, 256, 4), "256x2": (256, 2, 256, 2), "256x1": (256, 1, 256, 1),
         "512x4": (512, 4, 512, 4), "512x2": (512, 2, 512, 2), "512x1": (512, 1, 512, 1)}
 # arm = (enc block, enc K, dec block, dec K[, enc order, dec order]); order (efl_fxp_tune 17 / 18):
-# 0 2-D grid, 1 flat, 2 flat XCD-aware
+# 0 2-D grid, 1 flat, 2 flat XCD-aware, 3 persistent (7th field: its workgroups, efl_fxp_tune 19)
 if os.environ.get("BATCH_ARMS"):
     ARMS = {a.split(":")[0]: tuple(int(v) for v in a.split(":")[1].split(",")) for a in os.environ["BATCH_ARMS"].split(";")}
 dev = efl.lib.require_gpu()
@@ -42,7 +42,8 @@ for r in range(9):
     for a, arm in ARMS.items():
         eb, ek, db, dk = arm[:4]
         oe, od = arm[4:6] if len(arm) >= 6 else (0, 0)
-        for kind, v in ((10, eb), (11, ek), (12, db), (13, dk), (17, oe), (18, od)):
+        pg = arm[6] if len(arm) >= 7 else 2048
+        for kind, v in ((10, eb), (11, ek), (12, db), (13, dk), (17, oe), (18, od), (19, pg)):
             efl.lib.check(min(0, lib.efl_fxp_tune(kind, v)))
         for _ in range(3):
             step()

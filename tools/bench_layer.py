@@ -142,6 +142,8 @@ def party(role, my, peer, q, steps, warmup, kind):
         timer.wrap(layer_mod, "fixedpoint_encode", "fixedpoint_encode")
         timer.wrap(layer_mod, "_decrypt_decode", "decrypt+decode")
         timer.wrap(c, "_send_raw", "send (serialise, hex)", lambda name, t: _numel(t))
+        from efl.framework.communicator import SendHandle
+        timer.wrap(SendHandle, "result", "send (wait for the peer's recv)")
         timer.wrap(c, "_recv_raw", "recv (wait, parse)")
         timer.on = True
         t1 = time.perf_counter()

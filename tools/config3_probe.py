@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""BASELINE config 3 beside config 2 for profiling: `--reps` steps of the batched encode + decode over
+4096 separate 64 KiB fp32 slices (the bench's config3), then the same number of streaming steps over
+one 64 Mi-element tensor (the same bytes). Meant to run under rocprofv3 (kernel trace, or one PMC
+pass: FETCH_SIZE / WRITE_SIZE / SQ_* counters) so the batched and streaming kernels of one run can be
+compared per launch. Prints one JSON line (the round trip is checked)."""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "elastic-federated-learning-solution_amd"))
+import torch  # noqa: E402
+
+import efl  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--order", type=int, nargs=2, default=None, help="efl_fxp_tune 17 / 18 (batched tile order)")
+    a = ap.parse_args()
+    dev = efl.lib.require_gpu()
+    lib = efl.lib.raw()
+    if a.order:
+        lib.efl_fxp_tune(17, a.order[0])
+        lib.efl_fxp_tune(18, a.order[1])
+    S, N = 4096, 16384
+    g = torch.Generator(device=dev).manual_seed(1)
+    xs = [torch.randn(128, 128, device=dev, generator=g) * 0.01 for _ in range(S)]
+    Ms = [torch.empty(128, 128, dtype=torch.int64, device=dev) for _ in range(S)]
+    Es = [torch.empty(128, 128, dtype=torch.int64, device=dev) for _ in range(S)]
+    ys = [torch.empty(128, 128, device=dev) for _ in range(S)]
+    enc_t, dec_t = efl.lib.BatchTables(xs, Ms, Es), efl.lib.BatchTables(Ms, Es, ys)
+    sh = torch.cuda.current_stream().cuda_stream
+    for _ in range(a.reps):
+        efl.lib.encode_batched_into(enc_t, 1, False, sh)
+        efl.lib.decode_batched_into(dec_t, 1, 1, sh)
+    torch.cuda.synchronize()
+    ok = all(torch.equal(x, y) for x, y in zip(xs[::97], ys[::97]))
+    del Ms, Es, ys, enc_t, dec_t
+    x = torch.randn(S * N, device=dev, generator=g)
+    M = torch.empty(S * N, dtype=torch.int64, device=dev)
+    E = torch.empty_like(M)
+    y = torch.empty_like(x)
+    for _ in range(a.reps):
+        efl.lib.check(lib.efl_fxp_encode(x.data_ptr(), 1, M.data_ptr(), E.data_ptr(), S * N, 0, sh))
+        efl.lib.check(lib.efl_fxp_decode(M.data_ptr(), E.data_ptr(), y.data_ptr(), 1, S * N, S * N, 1, sh))
+    torch.cuda.synchronize()
+    print(json.dumps({"tool": "config3_probe", "version": efl.lib.version(), "reps": a.reps,
+                      "batched_roundtrip_ok": ok, "stream_roundtrip_ok": bool(torch.equal(x, y))}))
+
+
+if __name__ == "__main__":
+    main()

@@ -27,8 +27,22 @@ run() {
     layer)  timeout -k 10 400 python -u tools/bench_layer.py --steps 3 --warmup 1 > gpurun_out/r03_layer_dense.jsonl 2> gpurun_out/r03_layer_dense.err && \
             timeout -k 10 400 python -u tools/bench_layer.py --steps 3 --warmup 1 --kind weight > gpurun_out/r03_layer_weight.jsonl 2> gpurun_out/r03_layer_weight.err ;;
     e2ebench) timeout -k 10 600 python -u tools/bench_e2e.py > gpurun_out/r03_bench_e2e.json 2> gpurun_out/r03_bench_e2e.err ;;
-    bprobe) timeout -k 10 300 python -u tools/batched_probe.py > gpurun_out/r03_batched_probe.json 2> gpurun_out/r03_batched_probe.err ;;
+    bprobe) BATCH_ARMS="base:256,2,256,4,0,0;flat:256,2,256,4,1,1;p2048:256,2,256,4,3,3,2048;p4096:256,2,256,4,3,3,4096;p1024:256,2,256,4,3,3,1024;p8192:256,2,256,4,3,3,8192;pe_d0:256,2,256,4,3,0,4096;pe512:512,1,256,4,3,3,4096;pd2:256,2,256,2,3,3,4096" \
+            timeout -k 10 300 python -u tools/batched_probe.py > gpurun_out/r03_batched_probe.json 2> gpurun_out/r03_batched_probe.err ;;
     decfam) timeout -k 10 600 python -u tools/sweep_dec_family.py > gpurun_out/r03_dec_family.jsonl 2> gpurun_out/r03_dec_family.err ;;
+    c3kt)   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/r03_c3_kt -o run --output-format csv \
+              -- python3 tools/config3_probe.py --reps 20 > gpurun_out/r03_c3_kt.log 2>&1 && \
+            python tools/pmc_reduce.py /tmp/r03_c3_kt --match batched k_stream --prune > gpurun_out/r03_c3_kt.json && \
+            timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/r03_c3_kt_flat -o run --output-format csv \
+              -- python3 tools/config3_probe.py --reps 20 --order 1 1 > gpurun_out/r03_c3_kt_flat.log 2>&1 && \
+            python tools/pmc_reduce.py /tmp/r03_c3_kt_flat --match batched k_stream --prune > gpurun_out/r03_c3_kt_flat.json ;;
+    c3pmc)  for pass in "FETCH_SIZE" "WRITE_SIZE" \
+                        "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_SMEM SQ_INSTS_SALU SQ_WAVES SQ_INSTS_VMEM"; do
+              tag=$(echo $pass | cut -d' ' -f1)
+              timeout -s KILL 120 rocprofv3 --pmc $pass -d /tmp/r03_c3_$tag -o run --output-format csv \
+                -- python3 tools/config3_probe.py --reps 3 > gpurun_out/r03_c3_$tag.log 2>&1 || return $?
+              python tools/pmc_reduce.py /tmp/r03_c3_$tag --match batched k_stream --prune > gpurun_out/r03_c3_$tag.json || return $?
+            done ;;
     mask)   timeout -k 10 300 python -u tools/bench_mask.py > gpurun_out/r03_bench_mask.jsonl 2> gpurun_out/r03_bench_mask.err ;;
     *) echo "unknown step $1"; return 2 ;;
   esac
