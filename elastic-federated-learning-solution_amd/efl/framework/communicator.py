@@ -351,7 +351,7 @@ class Communicator(object):
         if hasattr(t, "to_hex"):                                  # CipherTensor: DT_STRING on the wire
             t = t.to_hex()
         if isinstance(t, HexTensor):
-            dtype, shape, content = wire.DT_STRING, t.shape, t.tensor_content_parts()
+            dtype, shape, content = wire.DT_STRING, t.shape, t.wire_parts()
         else:
             if not isinstance(t, torch.Tensor):
                 t = torch.as_tensor(np.asarray(t))

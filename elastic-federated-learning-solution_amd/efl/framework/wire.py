@@ -17,6 +17,7 @@ received content is returned as a zero-copy memoryview.
 """
 from __future__ import annotations
 
+import ctypes
 import struct
 
 import numpy as np
@@ -104,29 +105,75 @@ def shape_proto(shape) -> bytes:
     return bytes(out)
 
 
+def _nbytes(piece) -> int:
+    """Size of a payload piece: a bytes-like, or a contiguous uint8 torch tensor (e.g. text that
+    still lives in device memory)."""
+    if hasattr(piece, "is_cuda") and hasattr(piece, "numel"):
+        return int(piece.numel())
+    return memoryview(piece).nbytes
+
+
 def tensor_proto_parts(dtype: int, shape, content) -> list:
-    """Parts of a serialized TensorProto (content = bytes-like, or a tuple/list of bytes-likes
-    that together form tensor_content; not copied)."""
+    """Parts of a serialized TensorProto (content = bytes-like, or a tuple/list of bytes-likes /
+    uint8 torch tensors that together form tensor_content; not copied)."""
     sp = shape_proto(shape)
     parts = [key(1, _VARINT) + varint(dtype), _len_field(2, len(sp)) + sp]
     pieces = list(content) if isinstance(content, (tuple, list)) else [content]
-    n = sum(memoryview(c).nbytes for c in pieces)
+    n = sum(_nbytes(c) for c in pieces)
     if n:
         parts.append(_len_field(4, n))
         parts.extend(pieces)
     return parts
 
 
+_bytes_new = ctypes.pythonapi.PyBytes_FromStringAndSize
+_bytes_new.restype = ctypes.py_object
+_bytes_new.argtypes = [ctypes.c_void_p, ctypes.c_ssize_t]
+_bytes_addr = ctypes.pythonapi.PyBytes_AsString
+_bytes_addr.restype = ctypes.c_void_p
+_bytes_addr.argtypes = [ctypes.py_object]
+
+
+def _assemble(parts, total: int) -> bytes:
+    """One new `bytes` of `total` bytes filled with the parts in order — created uninitialised
+    through the C API (PyBytes_FromStringAndSize(NULL, n), then written before anything else sees
+    it, the documented way to build a bytes object in place), so each payload is copied exactly once
+    into the message gRPC takes: host pieces by memcpy, device pieces (torch uint8 tensors) by one
+    device-to-host copy straight into the message instead of into a host buffer that a join then
+    copies again."""
+    if total < 2:   # the interpreter shares its 0- and 1-byte objects: never write into those
+        return b"".join(bytes(p) if not hasattr(p, "is_cuda") else p.cpu().numpy().tobytes() for p in parts)
+    out = _bytes_new(None, total)
+    view = np.ctypeslib.as_array((ctypes.c_uint8 * total).from_address(_bytes_addr(out)))
+    pos = 0
+    for p in parts:
+        if hasattr(p, "is_cuda"):
+            n = int(p.numel())
+            if n:
+                import torch
+                torch.from_numpy(view[pos:pos + n]).copy_(p.reshape(-1))
+        else:
+            mv = memoryview(p).cast("B")
+            n = mv.nbytes
+            if n:
+                view[pos:pos + n] = np.frombuffer(mv, np.uint8)
+        pos += n
+    if pos != total:
+        raise ValueError("message parts do not add up to the message size")
+    return out
+
+
 def message_request(name: str, step: int, dtype: int, shape, content) -> bytes:
-    """Serialized MessageRequest{name, step, tensor}: one join, the payload copied once."""
+    """Serialized MessageRequest{name, step, tensor}: the payload copied once, into the message."""
     tparts = tensor_proto_parts(dtype, shape, content)
-    tlen = sum(memoryview(p).nbytes for p in tparts)
+    tlen = sum(_nbytes(p) for p in tparts)
     nb = name.encode()
     head = [_len_field(1, len(nb)) + nb]
     if step:
         head.append(key(2, _VARINT) + varint(step))
     head.append(_len_field(3, tlen))
-    return b"".join(head + tparts)
+    parts = head + tparts
+    return _assemble(parts, sum(_nbytes(p) for p in parts))
 
 
 class TensorMsg:

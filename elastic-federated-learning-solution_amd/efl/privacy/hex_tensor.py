@@ -138,6 +138,17 @@ class HexTensor:
         tensor_content, for a serialiser that joins them without another copy."""
         return _varint32_encode(self.offs[1:] - self.offs[:-1]), self.buf
 
+    def wire_parts(self):
+        """tensor_content_parts for the sender: when the text still lives only in device memory
+        (made by the hex kernels) the second part is that device uint8 tensor, which the message
+        assembly copies straight into the outgoing request (efl.framework.wire._assemble) — the
+        text is never staged in a host buffer of its own."""
+        if self._buf is None and self._dev is not None:
+            _, chars, _ = self._dev
+            total = int(self.offs[-1]) if self.numel() else 0
+            return _varint32_encode(self.offs[1:] - self.offs[:-1]), chars[:total]
+        return self.tensor_content_parts()
+
     def to_tensor_content(self) -> bytes:
         return b"".join(self.tensor_content_parts())
 

@@ -141,3 +141,28 @@ def test_response_matches_protobuf(code, msg):
     ours = wire.message_response(code, msg)
     assert ours == PB["MessageResponse"](code=code, msg=msg).SerializeToString()
     assert wire.parse_message_response(ours) == (code, msg)
+
+
+def test_message_assembled_in_place_from_mixed_parts():
+    """message_request builds the request in one new bytes object: host parts, torch uint8 tensors
+    (device text in production) and a split tensor_content give the same bytes as a plain join."""
+    import numpy as np
+    import torch
+    from efl.framework import wire
+    from efl.privacy.hex_tensor import HexTensor
+    hx = HexTensor.from_strings(["1f", "abcdef", "-3", "0" * 300])
+    head, text = hx.tensor_content_parts()
+    want = wire.message_request("x_[x]_mantissa", 7, wire.DT_STRING, hx.shape, bytes(head) + bytes(text))
+    got = wire.message_request("x_[x]_mantissa", 7, wire.DT_STRING, hx.shape, (head, torch.from_numpy(text.copy())))
+    assert isinstance(got, bytes) and got == want
+    got2 = wire.message_request("x_[x]_mantissa", 7, wire.DT_STRING, hx.shape, [memoryview(head), text])
+    assert got2 == want
+    # tiny messages never write into the interpreter's shared 0/1-byte objects
+    assert wire._assemble([b""], 0) == b"" and wire._assemble([b"a"], 1) == b"a"
+    t = torch.arange(10, dtype=torch.int64)
+    assert wire.message_request("t", 0, wire.DT_INT64, (10,), t.numpy()) == \
+        wire.message_request("t", 0, wire.DT_INT64, (10,), t.numpy().tobytes())
+    name, step, msg = wire.parse_message_request(got)
+    assert (name, step) == ("x_[x]_mantissa", 7)
+    assert HexTensor.from_tensor_content(msg.content, msg.shape).strings() == hx.strings()
+    assert np.array_equal(np.frombuffer(bytes(b"ab"), np.uint8), np.array([97, 98], np.uint8))

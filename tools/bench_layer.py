@@ -144,6 +144,13 @@ def party(role, my, peer, q, steps, warmup, kind):
         timer.wrap(c, "_send_raw", "send (serialise, hex)", lambda name, t: _numel(t))
         from efl.framework.communicator import SendHandle
         timer.wrap(SendHandle, "result", "send (wait for the peer's recv)")
+        # the pieces of a ciphertext send (exclusive: what is left under "send" is the gRPC hand-off)
+        from efl.privacy.paillier_cipher import CipherTensor
+        from efl.privacy.hex_tensor import HexTensor
+        from efl.framework import wire
+        timer.wrap(CipherTensor, "to_hex", "send: hex text (GPU)")
+        timer.wrap(HexTensor, "wire_parts", "send: varint lengths")
+        timer.wrap(wire, "message_request", "send: request assembly (text D2H into it)")
         timer.wrap(c, "_recv_raw", "recv (wait, parse)")
         timer.on = True
         t1 = time.perf_counter()

@@ -43,6 +43,8 @@ run() {
                 -- python3 tools/config3_probe.py --reps 3 > gpurun_out/r03_c3_$tag.log 2>&1 || return $?
               python tools/pmc_reduce.py /tmp/r03_c3_$tag --match batched k_stream --prune > gpurun_out/r03_c3_$tag.json || return $?
             done ;;
+    grpc)   timeout -k 10 300 python -u tools/grpc_raw_probe.py > gpurun_out/r03_grpc_raw.json 2>&1 && \
+            timeout -k 10 400 python -u tools/grpc_probe.py --mib 512 --reps 3 --channels 1 2 > gpurun_out/r03_grpc_probe2.jsonl 2>&1 ;;
     mask)   timeout -k 10 300 python -u tools/bench_mask.py > gpurun_out/r03_bench_mask.jsonl 2> gpurun_out/r03_bench_mask.err ;;
     *) echo "unknown step $1"; return 2 ;;
   esac
