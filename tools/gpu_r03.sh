@@ -13,7 +13,7 @@ run() {
     smoke)  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r03_smoke.log 2>&1 ;;
     bench)  timeout -k 10 300 python -u bench.py > gpurun_out/r03_bench.json 2> gpurun_out/r03_bench.err ;;
     prof)   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r03_prof_trace -o run --output-format csv \
-              -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/r03_prof_trace.log 2>&1 ;;
+              -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-extras > gpurun_out/r03_prof_trace.log 2>&1 ;;
     pmc)    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/r03_prof_fetch -o run --output-format csv \
               -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-extras > gpurun_out/r03_prof_fetch.log 2>&1 && \
             timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/r03_prof_write -o run --output-format csv \
