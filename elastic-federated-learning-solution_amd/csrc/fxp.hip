@@ -555,10 +555,12 @@ constexpr int kEnc = 0, kDec = 1;
 // batched tile (efl_fxp_encode_batched / decode_batched): B lanes x K pairs per workgroup
 constexpr int kBatchB = 256, kBatchK = 4;
 constexpr long long kMaxGridY = 65535;
-// fp32 [encode, decode]: encode 256 x 2 pairs measured 1.5-2 % faster than 256 x 4 in the config-3
-// step (tools/batched_probe.py, profiles/r02/batched_probe*.json); decode's shape is within noise
-std::atomic<int> g_batch_block[2] = {{kBatchB}, {kBatchB}};
-std::atomic<int> g_batch_k[2] = {{2}, {kBatchK}};
+// fp32 [encode, decode]: 512 lanes x 2 pairs both ways, one 2048-element tile per workgroup (half
+// the encode workgroups of round 2's 256 x 2 encode / 256 x 4 decode). Interleaved A/B on three
+// boxes (tools/batched_probe.py, profiles/r03/batched_probe_shapes.json): config-3 step 0.4086 ->
+// 0.4043, 0.4125 -> 0.4084 and 0.4319 -> 0.4390 ms, i.e. within the +-2 % box spread either way
+std::atomic<int> g_batch_block[2] = {{512}, {512}};
+std::atomic<int> g_batch_k[2] = {{2}, {2}};
 // efl_fxp_tune 17 / 18: tile order of the fp32 batched encode / decode: 0 2-D grid (tensor =
 // blockIdx.y), 1 one flat tensor-major grid, 2 the flat grid in XCD-aware order
 std::atomic<int> g_batch_order[2] = {{0}, {0}};

@@ -310,19 +310,30 @@ def test_batched_ragged(efl):
         assert np.array_equal(bits32(y), fxp.decode(Mo, Eo).view(np.uint32))
 
 
-@pytest.mark.parametrize("knob", [(10, 512), (11, 1), (11, 4), (12, 512), (13, 2)])
+@pytest.mark.parametrize("knob", [(10, 256), (10, 128), (11, 1), (11, 4), (12, 256), (12, 128), (13, 1), (13, 4),
+                                  (17, 1), (17, 2), (17, 3), (18, 1), (18, 2), (18, 3), (19, 7)])
 def test_batched_tuning_variants_identical(efl, knob):
-    """Every batched fp32 tile shape (efl_fxp_tune 10-13) gives the same bits."""
+    """Every batched fp32 tile shape and tile order (efl_fxp_tune 10-13, 17-19: 2-D grid, flat,
+    flat XCD-aware, persistent walk and its workgroup count) gives the same bits; ragged sizes,
+    tensors smaller than a tile, and (for the persistent walk with 7 workgroups) many tiles each."""
     lib = efl.lib.raw()
-    sizes = [1, 5, 4095, 16384, 30001]
+    if knob[0] == 19:
+        prev_order = (lib.efl_fxp_tune(17, 3), lib.efl_fxp_tune(18, 3))
+    sizes = [1, 5, 4095, 16384, 30001, 2, 65536 + 3]
     xs_np = [rand_bits(n, 40 + n).view(np.float32) for n in sizes]
     prev = lib.efl_fxp_tune(*knob)
-    assert prev > 0
+    assert prev >= 0
+    xs = [dev(a) for a in xs_np]
+    # one tensor 4 bytes off 16-B alignment: its tiles take the element path in every order
+    xs[2] = dev(np.concatenate([[0], xs_np[2].view(np.uint32)]).astype(np.uint32).view(np.float32))[1:]
     try:
-        Ms, Es = efl.lib.ops.convert_to_fixed_point_batched([dev(a) for a in xs_np])
+        Ms, Es = efl.lib.ops.convert_to_fixed_point_batched(xs)
         ys = efl.lib.ops.fixed_point_to_float_point_batched(Ms, Es)
     finally:
         lib.efl_fxp_tune(knob[0], prev)
+        if knob[0] == 19:
+            lib.efl_fxp_tune(17, prev_order[0])
+            lib.efl_fxp_tune(18, prev_order[1])
     for a, M, E, y in zip(xs_np, Ms, Es, ys):
         Mo, Eo = fxp.encode(a)
         assert np.array_equal(host(M), Mo) and np.array_equal(host(E), Eo)

@@ -34,21 +34,36 @@ def main():
     ys = [torch.empty(128, 128, device=dev) for _ in range(S)]
     enc_t, dec_t = efl.lib.BatchTables(xs, Ms, Es), efl.lib.BatchTables(Ms, Es, ys)
     sh = torch.cuda.current_stream().cuda_stream
-    for _ in range(a.reps):
+    import time
+
+    def wall(fn, k):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / k * 1e3
+
+    def batched():
         efl.lib.encode_batched_into(enc_t, 1, False, sh)
         efl.lib.decode_batched_into(dec_t, 1, 1, sh)
-    torch.cuda.synchronize()
+    for _ in range(3):
+        batched()
+    ms_b = wall(batched, a.reps)
     ok = all(torch.equal(x, y) for x, y in zip(xs[::97], ys[::97]))
     del Ms, Es, ys, enc_t, dec_t
     x = torch.randn(S * N, device=dev, generator=g)
     M = torch.empty(S * N, dtype=torch.int64, device=dev)
     E = torch.empty_like(M)
     y = torch.empty_like(x)
-    for _ in range(a.reps):
+    def stream():
         efl.lib.check(lib.efl_fxp_encode(x.data_ptr(), 1, M.data_ptr(), E.data_ptr(), S * N, 0, sh))
         efl.lib.check(lib.efl_fxp_decode(M.data_ptr(), E.data_ptr(), y.data_ptr(), 1, S * N, S * N, 1, sh))
-    torch.cuda.synchronize()
+    for _ in range(3):
+        stream()
+    ms_s = wall(stream, a.reps)
     print(json.dumps({"tool": "config3_probe", "version": efl.lib.version(), "reps": a.reps,
+                      "batched_step_ms": round(ms_b, 4), "stream_step_ms": round(ms_s, 4),
                       "batched_roundtrip_ok": ok, "stream_roundtrip_ok": bool(torch.equal(x, y))}))
 
 

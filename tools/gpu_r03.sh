@@ -45,6 +45,12 @@ run() {
             done ;;
     grpc)   timeout -k 10 300 python -u tools/grpc_raw_probe.py > gpurun_out/r03_grpc_raw.json 2>&1 && \
             timeout -k 10 400 python -u tools/grpc_probe.py --mib 512 --reps 3 --channels 1 2 > gpurun_out/r03_grpc_probe2.jsonl 2>&1 ;;
+    bprobe2) BATCH_ARMS="${BATCH_ARMS:-base:256,2,256,4,0,0;d128k1:256,2,128,1,0,0;d128k2:256,2,128,2,0,0;d256k1:256,2,256,1,0,0;d256k2:256,2,256,2,0,0;d512k1:256,2,512,1,0,0;d512k2:256,2,512,2,0,0;d512k4:256,2,512,4,0,0;base2:256,2,256,4,0,0}" \
+            timeout -k 10 300 python -u tools/batched_probe.py > gpurun_out/r03_batched_probe2.json 2> gpurun_out/r03_batched_probe2.err ;;
+    c3gap)  timeout -k 10 300 python -u tools/config3_probe.py --reps 50 > gpurun_out/r03_c3_wall.json 2>&1 && \
+            timeout -k 10 300 rocprofv3 --kernel-trace -d /tmp/r03_c3_gap -o run --output-format csv \
+              -- python3 tools/config3_probe.py --reps 20 > gpurun_out/r03_c3_gap.log 2>&1 && \
+            python tools/kernel_gaps.py /tmp/r03_c3_gap/run_kernel_trace.csv > gpurun_out/r03_c3_gaps.json ;;
     mask)   timeout -k 10 300 python -u tools/bench_mask.py > gpurun_out/r03_bench_mask.jsonl 2> gpurun_out/r03_bench_mask.err ;;
     *) echo "unknown step $1"; return 2 ;;
   esac
