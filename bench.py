@@ -240,9 +240,12 @@ STAGE_P_KEYS = [("example 1024-bit n, group_size 10", 128, 64, 10, 262144),
                 ("default 4096-bit n, group_size 1", 512, 256, 1, 65536)]
 
 
-def _mont_macs(L, squarings, multiplies):
-    """32x32 MACs of CIOS Montgomery products over L limbs: 2 L^2 per product."""
-    return 2 * L * L * (squarings + multiplies)
+def _mont_macs(L, squarings, multiplies, cios_squarings=False):
+    """Limb MACs of Montgomery products over L limbs: 2 L^2 per multiply; a squaring forms each cross
+    product once (L (L + 1) / 2) plus the L^2 of the reduction, as the one-lane kernels do (sliced28.h
+    sqr_fips1). cios_squarings counts 2 L^2 per squaring instead: what the multi-lane families issue."""
+    sq = 2 * L * L if cios_squarings else L * (L + 1) // 2 + L * L
+    return 2 * L * L * multiplies + sq * squarings
 
 
 DEC_WINDOW = 5     # csrc/paillier_sliced.hip kDecWin (efl_pl_tune(ln, 2, 1), the default)
@@ -335,8 +338,9 @@ def stage_p(args):
             fam = pc.kernel_slicing(k.ln, name == "decrypt")
             issued = macs
             if name == "decrypt" and fam:     # sliced decryption exponentiates in radix 2^28
-                L28 = pc.limbs28_total(k.ln, k.ln // fam)
-                issued = sum(_mont_macs(L28, sq, mul) for sq, mul in dec_ops)
+                G = k.ln // fam               # lanes per number: one-lane numbers square by product scanning
+                L28 = pc.limbs28_total(k.ln, G)
+                issued = sum(_mont_macs(L28, sq, mul, cios_squarings=G > 1) for sq, mul in dec_ops)
             if name == "encrypt" and k.desc.off_table28 >= 0:   # the radix-2^28 table serves encryption
                 issued = _mont_macs(k.desc.n2_28_len, 0, rows * (1 - 2.0 ** -W) + 1)
             res[name] = {"elements_per_s": round(per_s), "ms": round(times[name] * 1e3, 3),
@@ -446,6 +450,7 @@ def stage_p_matmul(args, efl, pc, kp, lib, sh, stream, dev):
             S *= 2
     # x R and its odd powers (1 squaring + 2^(w-1) - 1 products); combining the partials + conversion out
     products = u * v * (1 + (1 << (MATMUL_WINDOW - 1))) + (2 * S * u * w if S > 1 else 0)
+    squarings = u * v                          # of `products`: the x^2 of each odd-power table, the levels below
     for sp in range(S):
         j0, j1 = v * sp // S, v * (sp + 1) // S
         for sgn in (1, -1):
@@ -454,12 +459,15 @@ def stage_p_matmul(args, efl, pc, kp, lib, sh, stream, dev):
             top = np.where(mask[None, :, :], d + bits[None, :, :], 0).max(axis=1)    # [u, w]
             started = mask.any(axis=0)[None, :].repeat(u, axis=0)
             # squarings below the top level, multiplies less the first (a copy), one conversion out
-            products += int(np.maximum(top - 1, 0)[started].sum()) + u * int(nwin[mask].sum()) - int(started.sum())
+            lv = int(np.maximum(top - 1, 0)[started].sum())
+            squarings += lv
+            products += lv + u * int(nwin[mask].sum()) - int(started.sum())
             if S == 1:
                 products += int(started.sum())
     per_term = u * int((bits + pop)[nz].sum()) + int((d * nz[None, :, :]).sum()) + 2 * u * w
     L_issued = k.desc.n2_28_len if (fam and k.desc.off_table28 >= 0) else L
-    macs, issued = 2 * L * L * products, 2 * L_issued * L_issued * products
+    macs = _mont_macs(L, squarings, products - squarings)
+    issued = _mont_macs(L_issued, squarings, products - squarings, cios_squarings=G > 1)
     # the whole op as the layer calls it (kernel + z_neg^-1 + z_pos * z_neg^-1), then a plaintext
     # check of the first outputs: sum_j xm*ym*2^(xe+ye-min), exactly
     xct = pc.CipherTensor(X, (u, v), k)

@@ -679,7 +679,17 @@ using namespace efl;
 
 EFL_API const char* efl_last_error(void) { return t_err.c_str(); }
 
+namespace efl {
+// efl_fxp_tune(20, nb): Philox blocks per lane of the DP noise kernel (csrc/mask.hip; 1, 2, 4). 4:
+// 0.669 / 0.685 of 8 TB/s against 0.594 / 0.366 for one block on two boxes (profiles/r03/bench_mask*)
+std::atomic<int> g_dp_blocks{4};
+}  // namespace efl
+
 EFL_API int efl_fxp_tune(int kind, int value) {
+  if (kind == 20) {                 // DP noise kernel: Philox blocks per lane (csrc/mask.hip)
+    if (value != 1 && value != 2 && value != 4) return EFL_E_INVALID_ARGUMENT;
+    return g_dp_blocks.exchange(value);
+  }
   if (kind == 14 || kind == 15) {   // XCD-aware tile order, streaming fp32 encode / decode
     if (value != 0 && value != 1) return EFL_E_INVALID_ARGUMENT;
     return g_xcd_order[kind - 14].exchange(value);

@@ -18,10 +18,12 @@
 //
 // Every kernel is one streaming pass: read x once, write each output once. One lane owns four
 // consecutive elements (one Philox block, dwordx4 loads and stores). HBM-bound, no LDS, no MFMA.
+#include <atomic>
 #include <cmath>
 
 #include "common.h"
 #include "pl_common.h"
+#include "sincos_angle.h"
 
 // Every product and sum rounds on its own, as TF's separate ops (and numpy in the oracle) do:
 // hipcc contracts a*b+c into one FMA by default, which changes the last bit.
@@ -219,7 +221,7 @@ __device__ __forceinline__ void box_muller(uint32_t x0, uint32_t x1, float& f0, 
   const float v1 = (float)(2.0 * 3.14159265358979323846 * (double)u01(x1));
   const float r = sqrtf(-2.0f * logf(u1));
   float sn, cs;
-  sincosf(v1, &sn, &cs);
+  efl_sincos_angle(v1, &sn, &cs);   // v1 in [0, 2 pi]: <= 1 ulp of the rounded sin / cos (sincos_angle.h)
   f0 = sn * r;
   f1 = cs * r;
 }
@@ -242,31 +244,67 @@ __device__ __forceinline__ float dp_one(float v, float z, float sigma, float div
   return POW2 ? (v + n) * div : (v + n) / div;
 }
 
-template <int MODE, bool POW2>
+// One lane owns NB Philox blocks (4 elements each) kBlock lanes apart, so a wave's accesses stay
+// 64 x 16 contiguous bytes. Round 2 drew the normals first and then loaded x: every lane sat in
+// Box-Muller (logf, sincosf, a double product) with nothing in flight, 0.68 of 8 TB/s. Now the
+// loads of all of a lane's blocks are issued first and the normals computed while they travel.
+template <int MODE, bool POW2, int NB>
 __global__ __launch_bounds__(kBlock) void k_dp_noise(const float* x, float* o,   // in place allowed
                                                      long long n, uint64_t seed, uint64_t ctr0, float sigma,
                                                      float div) {
-  const long long g = (long long)blockIdx.x * kBlock + threadIdx.x;
-  const long long i0 = g * 4;
-  if (i0 >= n) return;
-  float z[4];
-  normal4(seed, ctr0 + (uint64_t)g, z);
-  if (i0 + 4 <= n) {
-    const f4 v = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + g);
-    f4 r;
+  const long long g0 = (long long)blockIdx.x * (kBlock * NB) + threadIdx.x;
+  if (g0 * 4 >= n) return;
+  if ((g0 + (long long)(NB - 1) * kBlock) * 4 + 4 <= n) {
+    f4 v[NB];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) r[j] = dp_one<MODE, POW2>(v[j], z[j], sigma, div);
-    stv(reinterpret_cast<f4*>(o) + g, r);
-  } else {
-    for (int j = 0; j < 4 && i0 + j < n; ++j) o[i0 + j] = dp_one<MODE, POW2>(x[i0 + j], z[j], sigma, div);
+    for (int b = 0; b < NB; ++b) v[b] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + g0 + b * kBlock);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const long long g = g0 + b * kBlock;
+      float z[4];
+      normal4(seed, ctr0 + (uint64_t)g, z);
+      f4 r;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[j] = dp_one<MODE, POW2>(v[b][j], z[j], sigma, div);
+      stv(reinterpret_cast<f4*>(o) + g, r);
+    }
+    return;
+  }
+  for (int b = 0; b < NB; ++b) {
+    const long long g = g0 + b * kBlock, i0 = g * 4;
+    if (i0 >= n) break;
+    float z[4];
+    normal4(seed, ctr0 + (uint64_t)g, z);
+    if (i0 + 4 <= n) {
+      const f4 v = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + g);
+      f4 r;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[j] = dp_one<MODE, POW2>(v[j], z[j], sigma, div);
+      stv(reinterpret_cast<f4*>(o) + g, r);
+    } else {
+      for (int j = 0; j < 4 && i0 + j < n; ++j) o[i0 + j] = dp_one<MODE, POW2>(x[i0 + j], z[j], sigma, div);
+    }
   }
 }
 
 unsigned grid_for(long long lanes) { return (unsigned)((lanes + kBlock - 1) / kBlock); }
 
+template <int MODE, bool POW2>
+void launch_dp(int nb, long long lanes, const float* x, float* o, long long n, uint64_t seed, uint64_t ctr0,
+               float sigma, float d, hipStream_t s) {
+  const unsigned g1 = grid_for(lanes);
+  if (nb == 1) k_dp_noise<MODE, POW2, 1><<<g1, kBlock, 0, s>>>(x, o, n, seed, ctr0, sigma, d);
+  else if (nb == 4) k_dp_noise<MODE, POW2, 4><<<(g1 + 3) / 4, kBlock, 0, s>>>(x, o, n, seed, ctr0, sigma, d);
+  else k_dp_noise<MODE, POW2, 2><<<(g1 + 1) / 2, kBlock, 0, s>>>(x, o, n, seed, ctr0, sigma, d);
+}
+
 bool lanes_ok(long long lanes) { return lanes / kBlock < (1ll << 31); }
 
 }  // namespace
+
+// efl_fxp_tune(20, nb): Philox blocks per lane of the DP noise kernel (defined in fxp.hip)
+extern std::atomic<int> g_dp_blocks;
+
 }  // namespace efl
 
 using namespace efl;
@@ -343,10 +381,10 @@ EFL_API int efl_dp_noise(const float* x, float* out, int64_t n, int mode, float 
   const bool pow2 = std::isfinite(divisor) && std::frexp(std::fabs(divisor), &ex) == 0.5f &&
                     std::isnormal(1.0f / divisor);
   const float d = pow2 ? 1.0f / divisor : divisor;   // exact for a power of two with a normal reciprocal
-  const unsigned grid = grid_for(lanes);
-  if (mode == 0 && pow2) k_dp_noise<0, true><<<grid, kBlock, 0, s>>>(x, out, n, seed, ctr0, sigma, d);
-  else if (mode == 0) k_dp_noise<0, false><<<grid, kBlock, 0, s>>>(x, out, n, seed, ctr0, sigma, d);
-  else if (pow2) k_dp_noise<1, true><<<grid, kBlock, 0, s>>>(x, out, n, seed, ctr0, sigma, d);
-  else k_dp_noise<1, false><<<grid, kBlock, 0, s>>>(x, out, n, seed, ctr0, sigma, d);
+  const int nb = g_dp_blocks.load(std::memory_order_relaxed);
+  if (mode == 0 && pow2) launch_dp<0, true>(nb, lanes, x, out, n, seed, ctr0, sigma, d, s);
+  else if (mode == 0) launch_dp<0, false>(nb, lanes, x, out, n, seed, ctr0, sigma, d, s);
+  else if (pow2) launch_dp<1, true>(nb, lanes, x, out, n, seed, ctr0, sigma, d, s);
+  else launch_dp<1, false>(nb, lanes, x, out, n, seed, ctr0, sigma, d, s);
   return hip_status(hipGetLastError(), "efl_dp_noise");
 }

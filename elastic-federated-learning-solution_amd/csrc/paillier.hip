@@ -955,16 +955,18 @@ bool g_slicing_set[4][2] = {};   // set explicitly through efl_pl_tune: used as 
 
 // Decryption family for n elements: the default (C = 32) unless the launch would give fewer than
 // 768 waves (3 per 4 SIMDs) of that family; then C = 8 (four times the lanes per element). Round 3
-// sweep of the current kernels (tools/sweep_dec_family.py, profiles/r03/dec_family.jsonl): 1024-bit
-// n at 32,768 elements 7.9 ms with C = 8, 8.1 with 16, 10.4 with 32, and at 50,176 C = 32 wins
-// (10.5 against 11.9 / 13.2); 2048-bit 16,384: 31.7 (C = 8) against 37.2 (32); 4096-bit 4,096: 90
-// against 143. C = 16 is never the fastest (at 2048 / 4096 bits it spills into its window loop and
-// runs 3-5x slower), so the sizing skips it; round 1's rule halved C step by step.
+// sweep (tools/sweep_dec_family.py, profiles/r03/dec_family.jsonl): 2048-bit 16,384: 31.7 (C = 8)
+// against 37.2 (32); 4096-bit 4,096: 90 against 143. C = 16 is never the fastest (at 2048 / 4096 bits
+// it spills into its window loop and runs 3-5x slower), so the sizing skips it; round 1's rule
+// halved C step by step. The 1024-bit key's C = 32 family holds a number in ONE lane and squares by
+// product scanning (sliced28.h sqr_fips1, 1.3-1.4x faster than its CIOS squaring), which moves its
+// crossover down to 384 waves: 32,768 elements 6.5 ms (C = 32) against 7.8 (C = 8), 16,384 6.4
+// against 5.9 (profiles/r03/dec_family_fips.jsonl).
 inline int decrypt_family(int ln, long long n) {
   const int C = slicing(ln, 1);
   if (!C || g_slicing_set[ln_index(ln)][1]) return C;
-  constexpr long long kFewWaves = 768ll * 64;   // lanes of 768 waves
-  if (C == 32 && n * (ln / 32) < kFewWaves && pl::sliced_available(ln, 8)) return 8;
+  const long long few_waves = (ln == 32 ? 384ll : 768ll) * 64;   // lanes
+  if (C == 32 && n * (ln / 32) < few_waves && pl::sliced_available(ln, 8)) return 8;
   return C;
 }
 

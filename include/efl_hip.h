@@ -76,7 +76,8 @@ const char* efl_last_error(void);
  * kind 16 = the streaming fp32 encode stores the exponent pair before the mantissa pair (0 / 1);
  * kinds 17 / 18 = tile order of the fp32 batched encode / decode (0 2-D grid, 1 one flat tensor-major
  * grid, 2 the flat grid in XCD-aware order, 3 a persistent walk of kind-19 workgroups that loads the
- * next tile while storing the current one); batched workgroup sizes 128, 256, 512.
+ * next tile while storing the current one); batched workgroup sizes 128, 256, 512; kind 20 =
+ * Philox blocks per lane of efl_dp_noise (1, 2, 4; default 4).
  * Returns the previous value or EFL_E_INVALID_ARGUMENT. */
 int efl_fxp_tune(int kind, int value);
 

@@ -1,0 +1,76 @@
+"""Accuracy of the DP noise kernel's sin / cos of the Box-Muller angle (csrc/sincos_angle.h), on the
+host: the header is plain C with every fused step an explicit fma, so gcc with -ffp-contract=off
+(the kernel file's own `#pragma clang fp contract(off)`) rounds exactly as the device does.
+
+Checked against the correctly rounded float of the double-precision libm sin / cos:
+* exhaustively over every angle the kernel can see, float(2 pi (double) u) for the 2^23 values
+  u = j 2^-23 that Uint32ToFloat produces (TF's random_distributions.h, oracle/mask.py);
+* over every 61st float of [0, 2 pi] (about 18 M arguments), for any caller with another angle.
+The bound is 1 ulp for both (OCML's general sincosf, which the kernel used before, is also within
+1 ulp); the normal's stated tolerance in tests/test_dp_gpu.py (4 ulp) covers log, sqrt and the
+products on top of it.
+"""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "elastic-federated-learning-solution_amd", "csrc")
+
+PROG = r"""
+#include <stdio.h>
+#include <stdint.h>
+#include <string.h>
+#include <stdlib.h>
+#include "sincos_angle.h"
+static int32_t ordered(float f) { int32_t i; memcpy(&i, &f, 4); return i < 0 ? (int32_t)0x80000000 - i : i; }
+static long worst_s, worst_c;
+static void check(float v) {
+  float s, c;
+  efl_sincos_angle(v, &s, &c);
+  const long ds = labs((long)ordered(s) - ordered((float)sin((double)v)));
+  const long dc = labs((long)ordered(c) - ordered((float)cos((double)v)));
+  if (ds > worst_s) worst_s = ds;
+  if (dc > worst_c) worst_c = dc;
+}
+int main(void) {
+  for (uint32_t j = 0; j < (1u << 23); ++j) {
+    const float u = (float)j * (1.0f / 8388608.0f);
+    check((float)(2.0 * 3.14159265358979323846 * (double)u));
+  }
+  printf("%ld %ld\n", worst_s, worst_c);
+  worst_s = worst_c = 0;
+  const float top = (float)(2.0 * 3.14159265358979323846);
+  uint32_t hi;
+  memcpy(&hi, &top, 4);
+  for (uint32_t b = 0; b <= hi; b += 61) {
+    float v;
+    memcpy(&v, &b, 4);
+    check(v);
+  }
+  check(top);
+  printf("%ld %ld\n", worst_s, worst_c);
+  return 0;
+}
+"""
+
+
+@pytest.fixture(scope="module")
+def result(tmp_path_factory):
+    d = tmp_path_factory.mktemp("sincos")
+    src, exe = d / "check.c", d / "check"
+    src.write_text(PROG)
+    subprocess.check_call(["gcc", "-O2", "-ffp-contract=off", "-I", CSRC, "-o", str(exe), str(src), "-lm"])
+    out = subprocess.check_output([str(exe)], timeout=300).decode().split("\n")
+    return [tuple(int(v) for v in line.split()) for line in out if line.strip()]
+
+
+def test_every_reachable_angle_within_1ulp(result):
+    ws, wc = result[0]
+    assert ws <= 1 and wc <= 1, f"sin {ws} ulp, cos {wc} ulp"
+
+
+def test_whole_range_sample_within_1ulp(result):
+    ws, wc = result[1]
+    assert ws <= 1 and wc <= 1, f"sin {ws} ulp, cos {wc} ulp"

@@ -58,6 +58,20 @@ cases = {
 }
 
 
+def _dp_blocks(nb, mode):
+    def run():
+        old = lib.efl_fxp_tune(20, nb)
+        rc = lib.efl_dp_noise(xp, p0, n, mode, 1.0 if mode == 0 else 1.1, 256.0, 7, 0, sh)
+        lib.efl_fxp_tune(20, old)
+        return rc
+    return run
+
+
+# efl_fxp_tune(20, nb): the DP noise kernel at 1 / 2 / 4 Philox blocks per lane (A/B of the default)
+for _nb in (1, 2, 4):
+    cases[f"dp_noise_elementwise_nb{_nb}"] = (8, _dp_blocks(_nb, 0))
+
+
 def cpu_sample(name, rows=1024):
     """The oracle (numpy, the reference's op chain) on the first `rows` rows; GiB/s of input."""
     from oracle import mask
@@ -93,6 +107,6 @@ for name, (bpe, fn) in cases.items():
             "GiB_per_s_plaintext": round(4 * n / (ms * 1e-3) / 2**30, 2),
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbs / PEAK_GBS, 4), "bytes_per_elem": bpe}}
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and "_nb" not in name:
         line["cpu_baseline"] = cpu_sample(name)
     print(json.dumps(line), flush=True)

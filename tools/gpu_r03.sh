@@ -10,6 +10,8 @@ run() {
   case "$1" in
     tests)  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
               > gpurun_out/r03_pytest.log 2>&1 ;;
+    pltests) timeout -k 10 600 python -u -m pytest tests/test_paillier_gpu.py tests/test_paillier_scalar_gpu.py tests/test_paillier_layer_gpu.py \
+              -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r03_pltests.log 2>&1 ;;
     smoke)  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r03_smoke.log 2>&1 ;;
     bench)  timeout -k 10 300 python -u bench.py > gpurun_out/r03_bench.json 2> gpurun_out/r03_bench.err ;;
     prof)   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r03_prof_trace -o run --output-format csv \
@@ -51,6 +53,7 @@ run() {
             timeout -k 10 300 rocprofv3 --kernel-trace -d /tmp/r03_c3_gap -o run --output-format csv \
               -- python3 tools/config3_probe.py --reps 20 > gpurun_out/r03_c3_gap.log 2>&1 && \
             python tools/kernel_gaps.py /tmp/r03_c3_gap/run_kernel_trace.csv > gpurun_out/r03_c3_gaps.json ;;
+    ovh)    timeout -k 10 300 python -u tools/op_overhead_probe.py > gpurun_out/r03_op_overhead.jsonl 2> gpurun_out/r03_op_overhead.err ;;
     mask)   timeout -k 10 300 python -u tools/bench_mask.py > gpurun_out/r03_bench_mask.jsonl 2> gpurun_out/r03_bench_mask.err ;;
     *) echo "unknown step $1"; return 2 ;;
   esac
