@@ -151,6 +151,15 @@ def party(role, my, peer, q, steps, warmup, kind):
         timer.wrap(CipherTensor, "to_hex", "send: hex text (GPU)")
         timer.wrap(HexTensor, "wire_parts", "send: varint lengths")
         timer.wrap(wire, "message_request", "send: request assembly (text D2H into it)")
+        sent = [0, 0]                  # serialised request bytes and messages this party sends
+        assemble = wire.message_request
+
+        def counted(*a, **kw):
+            r = assemble(*a, **kw)
+            sent[0] += len(r)
+            sent[1] += 1
+            return r
+        wire.message_request = counted
         timer.wrap(c, "_recv_raw", "recv (wait, parse)")
         timer.on = True
         t1 = time.perf_counter()
@@ -162,7 +171,8 @@ def party(role, my, peer, q, steps, warmup, kind):
                       "step_ms": round(wall * 1e3, 1), "instrumented_step_ms": round(inst * 1e3, 1),
                       "ops_ms": {k: round(v * 1e3, 2) for k, v in sorted(timer.total.items(), key=lambda kv: -kv[1])},
                       "attributed_frac": round(sum(timer.total.values()) / inst, 3),
-                      "calls": dict(timer.calls), "elements": dict(timer.elems)}, None))
+                      "calls": dict(timer.calls), "elements": dict(timer.elems),
+                      "wire": {"bytes_sent": sent[0], "messages_sent": sent[1]}}, None))
     except BaseException as e:  # pragma: no cover - reported to the parent
         import traceback
         q.put((role, None, traceback.format_exc()[-2000:]))
@@ -191,6 +201,13 @@ def main():
         p.join(timeout=60)
     if err:
         raise SystemExit(f"{err[0]} failed:\n{err[1]}")
+    # both directions' request bytes of the instrumented step against the slower party's step: the
+    # rate the step would need from the transport if nothing else took time
+    total = sum(out[r]["wire"]["bytes_sent"] for r in out)
+    step_s = max(out[r]["step_ms"] for r in out) / 1e3
+    for r in out:
+        out[r]["wire"]["both_directions_bytes"] = total
+        out[r]["wire"]["both_directions_GBs_over_step"] = round(total / step_s / 1e9, 3)
     for role in ("follower", "leader"):
         print(json.dumps({"bench": f"paillier_mnist {a.kind} layer step, two processes, 1024-bit key",
                           "shape": {"activations": [ROWS, FEATURES if a.kind == "dense" else UNITS], "units": UNITS},
