@@ -152,3 +152,28 @@ def test_float64_and_half_gradients_take_the_float32_noise(dp):
     assert torch.equal(gb, dp.dp_noise(xb.float(), 1, 1.0, 1.0, NoiseStream(12, 5)).to(torch.bfloat16))
     with pytest.raises(Exception, match="floating-point"):
         dp.dp_noise(torch.ones(4, dtype=torch.int32, device="cuda"), 0, 1.0, 1.0, NoiseStream(1, 0))
+
+
+@pytest.mark.parametrize("n", [1, 5, 1023, 1024, 4097, 262147, 1 << 20])
+def test_blocks_per_lane_layouts_agree(dp, n):
+    """efl_fxp_tune(20, nb): 1, 2 or 4 Philox blocks per lane give the same bits, in place too, for
+    sizes that leave every kind of ragged last workgroup (the kernel's full-tile and tail paths)."""
+    import efl
+    from efl.privacy.secret_sharing import NoiseStream
+    lib = efl.lib.raw()
+    x = torch.randn(n, generator=torch.Generator().manual_seed(n)).cuda()
+    outs = []
+    old = lib.efl_fxp_tune(20, 1)
+    try:
+        for nb in (1, 2, 4):
+            lib.efl_fxp_tune(20, nb)
+            outs.append(dp.dp_noise(x, 0, 1.3, 7.0, NoiseStream(11, 3)).cpu())
+            y = x.clone()
+            efl.lib.check(lib.efl_dp_noise(y.data_ptr(), y.data_ptr(), n, 1, 0.9, 256.0, 11, 3,
+                                           torch.cuda.current_stream().cuda_stream))
+            outs.append(y.cpu())
+    finally:
+        lib.efl_fxp_tune(20, old)
+    for a, b in ((outs[0], outs[2]), (outs[0], outs[4]), (outs[1], outs[3]), (outs[1], outs[5])):
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+    assert lib.efl_fxp_tune(20, 3) < 0      # only 1, 2, 4

@@ -54,6 +54,7 @@ run() {
               -- python3 tools/config3_probe.py --reps 20 > gpurun_out/r03_c3_gap.log 2>&1 && \
             python tools/kernel_gaps.py /tmp/r03_c3_gap/run_kernel_trace.csv > gpurun_out/r03_c3_gaps.json ;;
     ovh)    timeout -k 10 300 python -u tools/op_overhead_probe.py > gpurun_out/r03_op_overhead.jsonl 2> gpurun_out/r03_op_overhead.err ;;
+    grpcopt) timeout -k 10 600 python -u tools/grpc_options_probe.py > gpurun_out/r03_grpc_options.jsonl 2>&1 ;;
     mask)   timeout -k 10 300 python -u tools/bench_mask.py > gpurun_out/r03_bench_mask.jsonl 2> gpurun_out/r03_bench_mask.err ;;
     *) echo "unknown step $1"; return 2 ;;
   esac
