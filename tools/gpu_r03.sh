@@ -55,6 +55,11 @@ run() {
             python tools/kernel_gaps.py /tmp/r03_c3_gap/run_kernel_trace.csv > gpurun_out/r03_c3_gaps.json ;;
     ovh)    timeout -k 10 300 python -u tools/op_overhead_probe.py > gpurun_out/r03_op_overhead.jsonl 2> gpurun_out/r03_op_overhead.err ;;
     grpcopt) timeout -k 10 600 python -u tools/grpc_options_probe.py > gpurun_out/r03_grpc_options.jsonl 2>&1 ;;
+    c3lay)  timeout -k 10 300 python -u tools/config3_layout_probe.py > gpurun_out/r03_c3_layout.jsonl 2> gpurun_out/r03_c3_layout.err && \
+            PYTORCH_HIP_ALLOC_CONF=expandable_segments:True timeout -k 10 300 python -u tools/config3_layout_probe.py \
+              >> gpurun_out/r03_c3_layout.jsonl 2>> gpurun_out/r03_c3_layout.err ;;
+    c3arms) C3_ARMS="${C3_ARMS:-e512k1:512,1,512,2,0,0;e256k2:256,2,512,2,0,0;d128k1:512,2,128,1,0,0;flat:512,2,512,2,1,1;xcd:512,2,512,2,2,2;e512k4:512,4,512,4,0,0}" \
+            timeout -k 10 400 python -u tools/config3_layout_probe.py > gpurun_out/r03_c3_arms.jsonl 2> gpurun_out/r03_c3_arms.err ;;
     mask)   timeout -k 10 300 python -u tools/bench_mask.py > gpurun_out/r03_bench_mask.jsonl 2> gpurun_out/r03_bench_mask.err ;;
     *) echo "unknown step $1"; return 2 ;;
   esac
