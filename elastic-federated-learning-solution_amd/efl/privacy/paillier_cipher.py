@@ -116,17 +116,23 @@ def _limbs28_rows(vals, L: int, nbytes: int) -> np.ndarray:
     return (bits[:, :need].reshape(len(vals), L, 28).astype(np.uint32) * w).sum(axis=2, dtype=np.uint32)
 
 
-TABLE_MAX_ENTRIES = 1 << 18   # per key: 2^18 entries = 256 MiB of 4096-bit (8192-bit n^2) words
+# Device memory the fixed-base table of one key may take, both layouts (round 3; round 2 capped the
+# table at 2^18 entries whatever their size). A fresh-randomness encryption costs
+# ceil(a_bits / W) (1 - 2^-W) table products, so the widest window that fits is the fastest; the
+# lookups of a table larger than the 256 MB Infinity Cache are random HBM reads, and they still pay
+# (tools/table_window_probe.py, profiles/r03/table_window_*.jsonl): the examples' 1024-bit key
+# 53.9 -> 69.6 M encrypts/s from W = 12 to 16 (1.1 GiB table), the reference default 4096-bit key
+# 823 k -> 979 k/s from W = 10 to 12 (1.4 GiB). 1.5 GiB is about half a percent of a 288 GB HBM.
+TABLE_MAX_BYTES = 3 << 29
 
 
-def choose_table_window(a_bits: int, max_entries: int = TABLE_MAX_ENTRIES) -> int:
-    """Widest window W whose table (ceil(a_bits / W) rows x 2^W - 1 entries) stays within
-    max_entries: a fresh-randomness encryption costs ceil(a_bits / W) (1 - 2^-W) products, so the
-    widest affordable window is the fastest. 2048-bit a (the reference default) -> W = 10,
-    512-bit a (the examples) -> W = 12."""
+def choose_table_window(a_bits: int, entry_bytes: int, max_bytes: int = TABLE_MAX_BYTES) -> int:
+    """Widest window W <= 16 whose table (ceil(a_bits / W) rows x 2^W - 1 entries of entry_bytes:
+    the n^2 words of every layout the key keeps) fits max_bytes. 2048-bit a of a 4096-bit n (the
+    reference default) -> W = 12, 512-bit a of a 1024-bit n (the examples) -> W = 16."""
     best = 1
     for W in range(1, 17):
-        if -(-a_bits // W) * ((1 << W) - 1) > max_entries:
+        if -(-a_bits // W) * ((1 << W) - 1) * entry_bytes > max_bytes:
             break
         best = W
     return best
@@ -317,20 +323,19 @@ class KeyBlock:
         api_rows = a_bits // g + (1 if a_bits % g else 0)
         if api_rows * ((1 << g) - 1) * n2.bit_length() > MAX_TABLE_BITS:
             raise errors.ResourceExhaustedError("Memory usage exceeds a predefined threshold.")
-        W = int(table_window) if table_window else choose_table_window(a_bits)
+        # radix-2^28 copy of the table for the sliced family the n^2 kernels use (include/efl_hip.h)
+        fam = kernel_slicing(ln, False)
+        L28 = limbs28_total(2 * ln, 2 * ln // fam) if fam else 0
+        W = int(table_window) if table_window else choose_table_window(a_bits, 4 * (self.lc + L28))
         if not 1 <= W <= 16:
             raise errors.InvalidArgumentError("table_window must be in [1, 16]")
         cols = (1 << W) - 1
         rows = -(-a_bits // W)
         d.table_rows, d.table_cols, d.table_window = rows, cols, W
         self.table_window = W
-        # radix-2^28 copy for the sliced family the n^2 kernels use (include/efl_hip.h)
         d.off_table28 = -1
-        fam = kernel_slicing(ln, False)
-        L28 = 0
         if fam:
             G = 2 * ln // fam
-            L28 = limbs28_total(2 * ln, G)
             if rows * cols * L28 * 4 <= TABLE28_MAX_BYTES:
                 R28 = 1 << (28 * L28)
                 d.n2_28_len, d.table28_log2g = L28, G.bit_length() - 1

@@ -135,11 +135,15 @@ def test_product_does_not_import_oracle():
 
 
 def test_table_window_choice():
-    """choose_table_window: the widest window whose table fits 2^18 entries."""
-    from efl.privacy.paillier_cipher import choose_table_window, TABLE_MAX_ENTRIES
-    assert choose_table_window(2048) == 10        # reference default key: 4096-bit n, 2048-bit a
-    assert choose_table_window(512) == 12         # the examples' 1024-bit key
+    """choose_table_window: the widest window <= 16 whose table (both layouts) fits 1.5 GiB."""
+    from efl.privacy.paillier_cipher import choose_table_window, TABLE_MAX_BYTES, limbs28_total
+    # entry bytes: the n^2 words plus the radix-2^28 copy of the C = 32 family
+    entry = {n: 4 * (n // 16 + limbs28_total(n // 16, max(1, n // 16 // 32))) for n in (512, 1024, 2048, 4096)}
+    assert choose_table_window(2048, entry[4096]) == 12   # reference default key: 4096-bit n, 2048-bit a
+    assert choose_table_window(512, entry[1024]) == 16    # the examples' 1024-bit key
+    assert choose_table_window(1024, entry[2048]) == 14
     for a_bits in (1, 7, 64, 256, 513, 1024, 2048, 4096, 8192):
-        W = choose_table_window(a_bits)
-        assert -(-a_bits // W) * ((1 << W) - 1) <= TABLE_MAX_ENTRIES
-        assert W == 16 or -(-a_bits // (W + 1)) * ((1 << (W + 1)) - 1) > TABLE_MAX_ENTRIES
+        for eb in entry.values():
+            W = choose_table_window(a_bits, eb)
+            assert W == 1 or -(-a_bits // W) * ((1 << W) - 1) * eb <= TABLE_MAX_BYTES
+            assert W == 16 or -(-a_bits // (W + 1)) * ((1 << (W + 1)) - 1) * eb > TABLE_MAX_BYTES

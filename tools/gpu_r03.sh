@@ -60,6 +60,9 @@ run() {
               >> gpurun_out/r03_c3_layout.jsonl 2>> gpurun_out/r03_c3_layout.err ;;
     c3arms) C3_ARMS="${C3_ARMS:-e512k1:512,1,512,2,0,0;e256k2:256,2,512,2,0,0;d128k1:512,2,128,1,0,0;flat:512,2,512,2,1,1;xcd:512,2,512,2,2,2;e512k4:512,4,512,4,0,0}" \
             timeout -k 10 400 python -u tools/config3_layout_probe.py > gpurun_out/r03_c3_arms.jsonl 2> gpurun_out/r03_c3_arms.err ;;
+    tblw)   timeout -k 10 500 python -u tools/table_window_probe.py > gpurun_out/r03_table_window.jsonl 2> gpurun_out/r03_table_window.err ;;
+    tblw4)  timeout -k 10 500 python -u tools/table_window_probe.py --n-bytes 512 --a-bytes 256 --group 1 10 11 12 --sizes 65536 \
+              > gpurun_out/r03_table_window4096.jsonl 2> gpurun_out/r03_table_window4096.err ;;
     mask)   timeout -k 10 300 python -u tools/bench_mask.py > gpurun_out/r03_bench_mask.jsonl 2> gpurun_out/r03_bench_mask.err ;;
     *) echo "unknown step $1"; return 2 ;;
   esac
