@@ -677,11 +677,19 @@ __global__ __launch_bounds__(kEvBlock) void k_mmevents(const long long* __restri
   hdr[l] = make_int2(ok ? cnt : -1, ok ? (int)top : 0);
 }
 
-// x R mod n^2 and its odd powers (radix 2^28, Montgomery) for every x element:
-// entry e of element i at Xm + (i * kMatEntries + e) * (CP * G), lane g's slice at + g * CP
+// x R mod n^2 and its odd powers (radix 2^28, Montgomery) for every x element (row r, term j of
+// x [u, v]): entry e at Xm + mat_slot(j, e, r, u) * (CP * G), lane g's slice at + g * CP. Term-major,
+// then entry, then row: a k_matmul28 wave's groups are consecutive rows of one output column, so at
+// one event they read the same (term, entry) of consecutive rows — one contiguous span (round 2's
+// row-major [r][j][e] put consecutive rows v * 16 slots, 2 MB at the MNIST shape, apart).
+__device__ __forceinline__ long long mat_slot(long long j, int e, long long r, long long u) {
+  return (j * kMatEntries + e) * u + r;
+}
+
 template <int C, int G>
 __global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_tomont28(Key k, const uint32_t* __restrict__ X,
-                                                                         uint32_t* __restrict__ Xm, long long N) {
+                                                                         uint32_t* __restrict__ Xm, long long N,
+                                                                         int u, int v) {
   constexpr int L = C * G, E = kSlBlock / G;
   constexpr int C28 = s28::limbs_per_lane(L, G), L28 = C28 * G, CP = pad4<C28>();
   extern __shared__ uint32_t lds[];
@@ -693,7 +701,9 @@ __global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_tomon
   slice_uniform<C28>(m28, k.at(k.d.off_n2_28), g);
   const uint32_t minv28 = k.d.n2_minv28;
   to_mont28<C, G>(t, X + i * L, k, m28, B, E, g);
-  uint32_t* q = Xm + i * (long long)kMatEntries * (CP * G) + g * CP;
+  const long long r = i / v, jt = i % v;
+  uint32_t* q = Xm + mat_slot(jt, 0, r, u) * (CP * G) + g * CP;
+  const long long estride = (long long)u * (CP * G);   // entry e + 1 of the same element
   store28<C28>(q, t);
 #pragma unroll
   for (int j = 0; j < C28; ++j) x2[j] = t[j];
@@ -705,7 +715,7 @@ __global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_tomon
 #pragma unroll 1
   for (int e2 = 1; e2 < kMatEntries; ++e2) {
     s28::mont_mul<C28, G>(t, LdsElem{B, E}, m28, minv28, g);
-    store28<C28>(q + (long long)e2 * (CP * G), t);
+    store28<C28>(q + (long long)e2 * estride, t);
   }
 }
 
@@ -790,7 +800,7 @@ __global__ __launch_bounds__(kSlBlock, C >= 32 ? EFL_MAT_WAVES32 : EFL_MAT_WAVES
       } else if (listed) {
         if (ev_i < h.x && (long long)(ev >> kEvLevelShift) == b) {
           const int ent = (int)((ev >> 16) & 31u);
-          addr = (((long long)row * v + j0 + (int)(ev & 0xFFFFu)) * kMatEntries + ent) * (CP * G) + g * CP;
+          addr = mat_slot(j0 + (int)(ev & 0xFFFFu), ent, row, u) * (CP * G) + g * CP;
           if ((ev >> kEvNegBit) & 1u) {
             op = 3;
             copy = !started1;
@@ -814,7 +824,7 @@ __global__ __launch_bounds__(kSlBlock, C >= 32 ? EFL_MAT_WAVES32 : EFL_MAT_WAVES
           const long long y = yc[(long long)j * w];
           const uint64_t ay = y < 0 ? 0ull - (uint64_t)y : (uint64_t)y;
           const int ent = (int)(((ay >> p) & ((1ull << kMatWin) - 1ull)) >> 1);
-          addr = (((long long)row * v + j) * kMatEntries + ent) * (CP * G) + g * CP;
+          addr = mat_slot(j, ent, row, u) * (CP * G) + g * CP;
           if (y < 0) {
             op = 3;
             copy = !started1;
@@ -1341,7 +1351,7 @@ hipError_t run_matmul28(const Key& k, const uint32_t* X, const long long* xe, co
   }
   if (err == hipSuccess) {
     hipLaunchKernelGGL((k_tomont28<C, G>), dim3(grid_of(nx, G)), dim3(kSlBlock), (size_t)2 * L28 * E * 4, s, k, X, Xm,
-                       nx);
+                       nx, u, v);
     err = hipGetLastError();
   }
   if (err == hipSuccess) {
