@@ -1,4 +1,4 @@
-"""CPU, world_size 2 (gloo): the multi-GPU layout — shard ranges, key-material broadcast, and the
+"""CPU, world_size 2 and 4 (gloo): the multi-GPU layout — shard ranges, key-material broadcast, and the
 invariant that sharded results equal the single-process result (the codec is the CPU oracle here;
 on MI355X the same code runs over RCCL with the HIP ops)."""
 import os
@@ -37,6 +37,9 @@ def _worker(rank, world, port, out):
     M, E = fxp.encode(x[s:e].numpy())
     gathered = [None] * world
     dist.all_gather_object(gathered, (s, e, M, E))
+    # bench.py's max-over-ranks of (elapsed, t_enc, t_dec)
+    mx = edist.all_reduce_max([float(rank), -float(rank), 1.5])
+    assert mx == [float(world - 1), 0.0, 1.5]
     if rank == 0:
         Mfull = np.concatenate([g_[2] for g_ in gathered])
         Efull = np.concatenate([g_[3] for g_ in gathered])
@@ -47,14 +50,15 @@ def _worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_two_rank_gloo():
+@pytest.mark.parametrize("world", [2, 4])
+def test_multi_rank_gloo(world):
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
     ctx = tmp.get_context("spawn")
     q = ctx.Queue()
-    tmp.start_processes(_worker, args=(2, port, q), nprocs=2, join=True, start_method="spawn")
-    res = [q.get(timeout=60) for _ in range(2)]
+    tmp.start_processes(_worker, args=(world, port, q), nprocs=world, join=True, start_method="spawn")
+    res = [q.get(timeout=60) for _ in range(world)]
     assert all(r[0] == b"\x07" * 32 and r[1] == {"n": "abc", "hs": "12"} for r in res)
     assert any(r[2] is True for r in res)
 
