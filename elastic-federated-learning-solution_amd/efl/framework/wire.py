@@ -150,8 +150,8 @@ def _assemble(parts, total: int) -> bytes:
         if hasattr(p, "is_cuda"):
             n = int(p.numel())
             if n:
-                import torch
-                torch.from_numpy(view[pos:pos + n]).copy_(p.reshape(-1))
+                from efl import staging
+                staging.to_host_into(view[pos:pos + n], p)
         else:
             mv = memoryview(p).cast("B")
             n = mv.nbytes

@@ -15,6 +15,8 @@ import warnings
 import numpy as np
 import torch
 
+from efl import staging
+
 
 class HexTensor:
     __slots__ = ("_buf", "_offs", "shape", "_dev")
@@ -72,14 +74,14 @@ class HexTensor:
         return (self._offs.size if self._offs is not None else int(self._dev[2].numel())) - 1
 
     def device_buffers(self, device):
-        """(chars uint8, offsets int64) on `device` (copied once, cached). A read-only host buffer
-        (a view of received message bytes) goes to the device without a host copy first."""
+        """(chars uint8, offsets int64) on `device` (copied once, cached). A host buffer (e.g. a
+        read-only view of received message bytes) goes through the pinned staging buffer."""
         if self._dev is None or self._dev[0] != device:
             host = self.buf if self.buf.size else np.zeros(1, np.uint8)
             with warnings.catch_warnings():
                 warnings.simplefilter("ignore", UserWarning)   # torch cannot mark the view read-only
-                chars = torch.from_numpy(host).to(device, copy=True)
-                offs = torch.from_numpy(self.offs).to(device, copy=True)
+                chars = staging.to_device(host, device)
+                offs = staging.to_device(self.offs, device)
             self._dev = (device, chars, offs)
         return self._dev[1], self._dev[2]
 
