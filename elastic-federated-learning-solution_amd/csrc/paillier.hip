@@ -208,6 +208,119 @@ __global__ __launch_bounds__(kPlBlock) void k_fbpowm(Key k, const uint32_t* __re
   store_g<LC>(out + i * LC, acc);
 }
 
+// z (2 L + 1 words) += f y for a uniform L-word f and a register L-word y, row R onwards. The rows
+// are a template recursion so every index is a compile-time constant (a fully unrolled L x L
+// nest leaves z in scratch).
+template <int L, int R>
+__device__ __forceinline__ void add_product(uint32_t (&z)[2 * L + 1], const uint32_t (&y)[L],
+                                            const uint32_t* __restrict__ f, uint32_t over = 0) {
+  if constexpr (R < L) {
+    const uint32_t fr = f[R];
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      const uint64_t p = mad(fr, y[j], (uint64_t)z[R + j] + c);
+      z[R + j] = (uint32_t)p;
+      c = (uint32_t)(p >> 32);
+    }
+    const uint64_t t = (uint64_t)z[R + L] + c + over;   // over: carry out of word R + L - 1's row
+    z[R + L] = (uint32_t)t;
+    add_product<L, R + 1>(z, y, f, (uint32_t)(t >> 32));
+  } else {
+    z[2 * L] += over;
+  }
+}
+
+// CRT join (efl_pl_crt_join): z = q^2 yp + p^2 yq mod n^2 for yp < p^2, yq < q^2 ([N][LN] words,
+// LN = the key's ln; z [N][2 LN]). With yp = x (q^2)^-1 mod p^2 and yq = x (p^2)^-1 mod q^2, z is x
+// mod n^2 (z = x mod p^2 and mod q^2). The key owner's encryption gets yp and yq straight from the
+// fixed-base walks mod p^2 and mod q^2, whose accumulators start from (q^2)^-1 and (p^2)^-1 instead
+// of 1 (KeyBlock walk_start), so the join is two plain LN x LN products, a sum and at most one
+// subtraction of n^2 — no modular product. One lane per element, the operand in registers; the sum
+// (2 LN + 1 words: q^2 yp + p^2 yq < 2 n^2) in registers for LN <= 32 (at LN = 64 that takes 766
+// registers and spills), else row by row into the lane's LDS column.
+template <int LN>
+__global__ __launch_bounds__(kPlBlock) void k_crt_join(Key k, const uint32_t* __restrict__ yp,
+                                                       const uint32_t* __restrict__ yq,
+                                                       uint32_t* __restrict__ out, long long N) {
+  extern __shared__ uint32_t lds[];
+  const int S = blockDim.x;
+  uint32_t* zcol = lds + threadIdx.x;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  if constexpr (LN <= 32) {
+    // the sum in registers (2 LN + 1 words), both products fully unrolled: no LDS round trips
+    uint32_t z[2 * LN + 1], y[LN];
+#pragma unroll
+    for (int j = 0; j <= 2 * LN; ++j) z[j] = 0u;
+    load_g<LN>(y, yp + i * LN);
+    add_product<LN, 0>(z, y, k.at(k.d.off_q2));
+    load_g<LN>(y, yq + i * LN);
+    add_product<LN, 0>(z, y, k.at(k.d.off_p2));
+    const uint32_t* n2 = k.at(k.d.off_n2);
+    uint32_t borrow = 0;
+#pragma unroll
+    for (int j = 0; j < 2 * LN; ++j) borrow = (uint32_t)(((uint64_t)z[j] - n2[j] - borrow) >> 63);
+    const bool ge = z[2 * LN] >= borrow;
+    borrow = 0;
+#pragma unroll
+    for (int j = 0; j < 2 * LN; ++j) {
+      const uint64_t d = (uint64_t)z[j] - (ge ? n2[j] : 0u) - borrow;
+      z[j] = (uint32_t)d;
+      borrow = (uint32_t)(d >> 63);
+    }
+    uint32_t zz[2 * LN];
+#pragma unroll
+    for (int j = 0; j < 2 * LN; ++j) zz[j] = z[j];
+    store_g<2 * LN>(out + i * (2 * LN), zz);
+    return;
+  }
+#pragma unroll 4
+  for (int j = 0; j <= 2 * LN; ++j) zcol[j * S] = 0u;
+  uint32_t y[LN];
+#pragma unroll 1
+  for (int pass = 0; pass < 2; ++pass) {
+    load_g<LN>(y, (pass ? yq : yp) + i * LN);
+    const uint32_t* f = k.at(pass ? k.d.off_p2 : k.d.off_q2);
+    uint32_t over = 0;   // carry out of word r + LN of the previous row
+#pragma unroll 1
+    for (int r = 0; r < LN; ++r) {
+      asm volatile("" ::: "memory");
+      const uint32_t fr = f[r];
+      uint32_t c = 0;
+#pragma unroll
+      for (int j = 0; j < LN; ++j) {
+        const uint64_t p = mad(fr, y[j], (uint64_t)zcol[(r + j) * S] + c);
+        zcol[(r + j) * S] = (uint32_t)p;
+        c = (uint32_t)(p >> 32);
+      }
+      const uint64_t t = (uint64_t)zcol[(r + LN) * S] + c + over;
+      zcol[(r + LN) * S] = (uint32_t)t;
+      over = (uint32_t)(t >> 32);
+    }
+    zcol[2 * LN * S] += over;
+  }
+  // z >= n^2 ? z - n^2 : z
+  const uint32_t* n2 = k.at(k.d.off_n2);
+  uint32_t borrow = 0;
+#pragma unroll 4
+  for (int j = 0; j < 2 * LN; ++j) borrow = (uint32_t)(((uint64_t)zcol[j * S] - n2[j] - borrow) >> 63);
+  const bool ge = zcol[2 * LN * S] >= borrow;   // word 2 LN is 0 or 1
+  borrow = 0;
+  uint32_t* o = out + i * (2 * LN);
+#pragma unroll 2
+  for (int j = 0; j < 2 * LN; j += 4) {
+    uint32_t w[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const uint64_t d = (uint64_t)zcol[(j + t) * S] - (ge ? n2[j + t] : 0u) - borrow;
+      w[t] = (uint32_t)d;
+      borrow = (uint32_t)(d >> 63);
+    }
+    *reinterpret_cast<uint4*>(o + j) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
 // m_x(c) = L_x(c^(x-1) mod x^2) * h mod x   (paillier.cc:39-48), x = p or q.
 // lo/hi: the 2*LP limbs of c (consumed). Result: LH limbs.
 template <int LP>
@@ -1101,6 +1214,23 @@ EFL_API int efl_pl_fbpowm(const void* key_block, const efl_pl_key* key, const ui
                       : dispatch_ln<RunFbpowm>(key->ln, k, a, hsa, (long long)n, seed, (long long)counter_base,
                                                (hipStream_t)stream),
                     "efl_pl_fbpowm");
+}
+
+EFL_API int efl_pl_crt_join(const void* key_block, const efl_pl_key* key, const uint32_t* xp, const uint32_t* xq,
+                            uint32_t* z, int64_t n, void* stream) {
+  if (!key_ok(key, true, 128)) return key && !key->has_private ? EFL_E_ABORTED : EFL_E_INVALID_ARGUMENT;
+  if (n <= 0) return n < 0 ? EFL_E_INVALID_ARGUMENT : EFL_OK;
+  Key k{(const uint32_t*)key_block, *key};
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned g = grid_of((long long)n);
+  const size_t lds = (size_t)(2 * key->ln + 1) * kPlBlock * 4;
+  switch (key->ln) {
+    case 16: hipLaunchKernelGGL((k_crt_join<16>), dim3(g), dim3(kPlBlock), lds, s, k, xp, xq, z, (long long)n); break;
+    case 32: hipLaunchKernelGGL((k_crt_join<32>), dim3(g), dim3(kPlBlock), lds, s, k, xp, xq, z, (long long)n); break;
+    case 64: hipLaunchKernelGGL((k_crt_join<64>), dim3(g), dim3(kPlBlock), lds, s, k, xp, xq, z, (long long)n); break;
+    default: hipLaunchKernelGGL((k_crt_join<128>), dim3(g), dim3(kPlBlock), lds, s, k, xp, xq, z, (long long)n); break;
+  }
+  return hip_status(hipGetLastError(), "efl_pl_crt_join");
 }
 
 EFL_API int efl_pl_decrypt(const void* key_block, const efl_pl_key* key, const uint32_t* ciphertext,

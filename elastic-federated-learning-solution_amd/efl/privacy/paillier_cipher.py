@@ -52,6 +52,7 @@ _PK = ctypes.POINTER(PlKey)
 for _name, _args in {
     "efl_pl_encrypt": [_vp, _PK, _vp, _vp, _vp, _i64, _u64, _i64, _vp],
     "efl_pl_fbpowm": [_vp, _PK, _vp, _vp, _i64, _u64, _i64, _vp],
+    "efl_pl_crt_join": [_vp, _PK, _vp, _vp, _vp, _i64, _vp],
     "efl_pl_decrypt": [_vp, _PK, _vp, _vp, _vp, _i64, _vp],
     "efl_pl_add": [_vp, _PK, _vp, _vp, _vp, _i64, _vp],
     "efl_pl_powm": [_vp, _PK, _vp, _vp, _i32, _vp, _i64, _vp],
@@ -241,7 +242,9 @@ class KeyBlock:
     """Host derivation + device upload of every constant the kernels read (efl_pl_key)."""
 
     def __init__(self, n: int, hs: int, a_bits: int, group_size: int, p=None, q=None, device=None,
-                 table_window=None, reuse_table=None):
+                 table_window=None, reuse_table=None, walk_start=None):
+        """walk_start: the fixed-base walk's accumulator starts from walk_start (mod n^2) instead of 1,
+        so efl_pl_fbpowm gives walk_start * hs^(a') mod n^2 (the CRT keys of crt_keys)."""
         if n.bit_length() < 128:
             raise errors.UnimplementedError("n of fewer than 128 bits is not supported on the GPU")
         if p is not None and q is not None and q >= 2 * p:
@@ -376,8 +379,45 @@ class KeyBlock:
             d.off_table28 = head.numel() + t32.numel()
             parts.append(t28.reshape(-1))
         self.block = torch.cat(parts)
+        if walk_start is not None:   # after the table build, which multiplies by the true R mod n^2
+            s0 = walk_start % n2
+            self.block[d.off_n2_one:d.off_n2_one + self.lc] = \
+                torch.from_numpy(_limbs(s0 * Rc % n2, self.lc).view(np.int32)).to(self.device)
+            if L28:
+                self.block[d.off_n2_one28:d.off_n2_one28 + L28] = \
+                    torch.from_numpy(_limbs28(s0 * (1 << (28 * L28)) % n2, L28).view(np.int32)).to(self.device)
         self.ptr = self.block.data_ptr()
+        # the key owner's CRT encryption keys (crt_keys), carried over when only the private part
+        # was set again
+        self._crt = None
+        if src is not None and getattr(src, "_crt", None) and (src.p, src.q) == (self.p, self.q) \
+                and (src.hs, src.a_bits, src.group_size) == (hs, a_bits, group_size) \
+                and torch.device(src.device) == torch.device(self.device):
+            self._crt = src._crt
         torch.cuda.current_stream(self.device).synchronize()
+
+    def crt_keys(self):
+        """The key owner's encryption keys: (KeyBlock of (p, hs mod p^2), KeyBlock of (q, hs mod
+        q^2)), built on first use. hs^(a') mod n^2 is then two fixed-base exponentiations on
+        half-length moduli (a quarter of the limb products each) and one CRT join
+        (efl_pl_crt_join): the same value, bit for bit, as the public-key path. None without the
+        private key, with EFL_PL_CRT_ENCRYPT=0, or when p and q are not half-length primes of a
+        supported limb class (512-bit n: 256-bit primes)."""
+        if self._crt is None:
+            self._crt = False
+            if self.desc.has_private and os.environ.get("EFL_PL_CRT_ENCRYPT", "1") != "0":
+                subs = []
+                p2, q2 = self.p * self.p, self.q * self.q
+                for x, start in ((self.p, pow(q2, -1, p2)), (self.q, pow(p2, -1, q2))):
+                    ln_x = next((c for c in _LIMB_CLASSES if 32 * c >= x.bit_length()), None)
+                    if ln_x is None or 2 * ln_x != self.ln:
+                        return None
+                    # the walk mod p^2 yields hs^(a') (q^2)^-1, mod q^2 hs^(a') (p^2)^-1: the join
+                    # z = q^2 yp + p^2 yq mod n^2 then needs no modular product
+                    subs.append(KeyBlock(x, self.hs % (x * x), self.a_bits, self.group_size, device=self.device,
+                                         walk_start=start))
+                self._crt = tuple(subs)
+        return self._crt or None
 
     def _build_table(self, hs, n2, W, rows, cols, head, r_one, r28_one, L28, chunk_entries=1 << 16):
         """T[i][j-1] = hs^(j 2^(W i)) mod n^2 for j in 1..2^W-1, in Montgomery form (x R mod n^2,
@@ -555,6 +595,10 @@ def philox_key(seed: bytes | int | None = None) -> int:
 class PaillierKeypair(object):
     """paillier.py:53-104 over the PaillierKeypair resource (paillier.cc:50-331)."""
 
+    # the key owner's fresh-randomness encryption and fbpowm go through CRT (KeyBlock.crt_keys);
+    # False (or EFL_PL_CRT_ENCRYPT=0) keeps them on n^2 as the reference does. Same ciphertexts.
+    crt_encrypt = True
+
     def __init__(self, seed: bytes | int | None = None):
         self._key: KeyBlock | None = None
         self._n_bytes = None
@@ -623,6 +667,25 @@ class PaillierKeypair(object):
         return CipherTensor(limbs, hx.shape, k)
 
     # -- ops -----------------------------------------------------------------------------
+    def _fresh_hsa(self, n, counter_base, a_dev=None):
+        """hs^(a') mod n^2 ([n, 2 ln] limbs) for the Philox draws at counters counter_base + i (or
+        the given exponents a_dev) by CRT, when this keypair holds the private key (KeyBlock.crt_keys);
+        None otherwise."""
+        k = self.key
+        subs = k.crt_keys() if self.crt_encrypt else None
+        if subs is None or n == 0:
+            return None
+        sh = _stream(k.device)
+        parts = []
+        for sk in subs:
+            x = torch.empty((n, sk.lc), dtype=torch.int32, device=k.device)
+            _efl_lib.check(_lib.efl_pl_fbpowm(*sk.args(), a_dev.data_ptr() if a_dev is not None else None,
+                                              x.data_ptr(), n, self.seed, counter_base, sh))
+            parts.append(x)
+        z = torch.empty((n, k.lc), dtype=torch.int32, device=k.device)
+        _efl_lib.check(_lib.efl_pl_crt_join(*k.args(), parts[0].data_ptr(), parts[1].data_ptr(), z.data_ptr(), n, sh))
+        return z
+
     def encrypt(self, plaintext, hsa=None, counter_base=None):
         """PaillierEncrypt (paillier.cc:443-503). hsa None (or all "0") draws a fresh a per element
         from Philox(seed, counter); counter_base defaults to a running per-keypair counter."""
@@ -649,6 +712,9 @@ class PaillierKeypair(object):
         ctr = self.counter if counter_base is None else int(counter_base)
         if counter_base is None:
             self.counter += N
+        if hsa_limbs is None:
+            hsa_limbs = self._fresh_hsa(N, ctr)   # the key owner: hs^(a') by CRT, same bits
+            zero_idx = None
         _efl_lib.check(_lib.efl_pl_encrypt(*k.args(), m.data_ptr(),
                                            hsa_limbs.data_ptr() if hsa_limbs is not None else None,
                                            out.data_ptr(), N, self.seed, ctr, _stream(k.device)))
@@ -659,8 +725,10 @@ class PaillierKeypair(object):
             sub = torch.empty((idx.numel(), k.lc), dtype=torch.int32, device=k.device)
             msub = m[idx].contiguous()
             for j0, j1, c0 in _counter_runs(zero_idx):
-                _efl_lib.check(_lib.efl_pl_encrypt(*k.args(), msub[j0:j1].data_ptr(), None, sub[j0:j1].data_ptr(),
-                                                   j1 - j0, self.seed, ctr + c0, _stream(k.device)))
+                h = self._fresh_hsa(j1 - j0, ctr + c0)
+                _efl_lib.check(_lib.efl_pl_encrypt(*k.args(), msub[j0:j1].data_ptr(), h.data_ptr() if h is not None else None,
+                                                   sub[j0:j1].data_ptr(), j1 - j0, self.seed, ctr + c0,
+                                                   _stream(k.device)))
             out[idx] = sub
         return PaillierTensor(self, CipherTensor(out, shape, k))
 
@@ -683,9 +751,11 @@ class PaillierKeypair(object):
                 raise errors.InvalidArgumentError("exponent wider than the fixed-base table")
             arr = np.stack([_limbs(v, words) for v in a]) if n else np.zeros((0, words), "<u4")
             a_dev = torch.from_numpy(arr.view(np.int32)).to(k.device)
-        out = torch.empty((n, k.lc), dtype=torch.int32, device=k.device)
-        _efl_lib.check(_lib.efl_pl_fbpowm(*k.args(), a_dev.data_ptr() if a is not None else None,
-                                          out.data_ptr(), n, self.seed, counter_base, _stream(k.device)))
+        out = self._fresh_hsa(n, counter_base, a_dev if a is not None else None)
+        if out is None:
+            out = torch.empty((n, k.lc), dtype=torch.int32, device=k.device)
+            _efl_lib.check(_lib.efl_pl_fbpowm(*k.args(), a_dev.data_ptr() if a is not None else None,
+                                              out.data_ptr(), n, self.seed, counter_base, _stream(k.device)))
         return CipherTensor(out, (n,), k)
 
     def decrypt(self, paillier_tensor, dtype="string"):

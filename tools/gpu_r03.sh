@@ -12,6 +12,12 @@ run() {
               > gpurun_out/r03_pytest.log 2>&1 ;;
     pltests) timeout -k 10 600 python -u -m pytest tests/test_paillier_gpu.py tests/test_paillier_scalar_gpu.py tests/test_paillier_layer_gpu.py \
               -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r03_pltests.log 2>&1 ;;
+    crt)    timeout -k 10 600 python -u -m pytest tests/test_paillier_crt_gpu.py tests/test_paillier_gpu.py -m gpu -x -v --timeout 300 \
+              --timeout-method thread > gpurun_out/r03_crt.log 2>&1 ;;
+    crtp)   timeout -k 10 300 python -u tools/crt_probe.py > gpurun_out/r03_crt_probe.jsonl 2> gpurun_out/r03_crt_probe.err && \
+            timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/r03_crt_kt -o run --output-format csv \
+              -- python3 tools/crt_probe.py --reps 3 > gpurun_out/r03_crt_kt.log 2>&1 && \
+            cp /tmp/r03_crt_kt/run_kernel_stats.csv gpurun_out/r03_crt_kernel_stats.csv ;;
     smoke)  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r03_smoke.log 2>&1 ;;
     bench)  timeout -k 10 300 python -u bench.py > gpurun_out/r03_bench.json 2> gpurun_out/r03_bench.err ;;
     prof)   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r03_prof_trace -o run --output-format csv \
