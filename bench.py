@@ -318,14 +318,13 @@ def stage_p(args):
         fns = [("encrypt", enc), ("decrypt", dec)]
         if subs:
             xs = [torch.empty((N, sk.lc), dtype=torch.int32, device=dev) for sk in subs]
-            hsa = torch.empty((N, k.lc), dtype=torch.int32, device=dev)
             ct_crt = torch.empty_like(ct)
 
             def enc_crt():
                 for sk, x in zip(subs, xs):
                     efl.lib.check(lib.efl_pl_fbpowm(*sk.args(), None, x.data_ptr(), N, 7, 0, sh))
-                efl.lib.check(lib.efl_pl_crt_join(*k.args(), xs[0].data_ptr(), xs[1].data_ptr(), hsa.data_ptr(), N, sh))
-                efl.lib.check(lib.efl_pl_encrypt(*k.args(), m.data_ptr(), hsa.data_ptr(), ct_crt.data_ptr(), N, 7, 0, sh))
+                efl.lib.check(lib.efl_pl_crt_join(*k.args(), xs[0].data_ptr(), xs[1].data_ptr(), m.data_ptr(),
+                                                  ct_crt.data_ptr(), N, sh))
             fns.append(("encrypt_crt", enc_crt))
         times = {}
         for name, fn in fns:
@@ -396,8 +395,8 @@ def stage_p(args):
 
 def stage_p_crt(k, subs, a_bytes, N, t, t_public, t_setup):
     """The key owner's encryption by CRT: algorithmic limb MACs = the two half-length fixed-base
-    walks (one product per non-zero window of each sub-table, + the conversion out) + the join (the
-    plain products q^2 yp and p^2 yq) + g(m) hsa mod n^2."""
+    walks (one product per non-zero window of each sub-table) + the join (the plain products q^2 yp
+    and p^2 yq) + one product mod n^2 (g(m) times the join's hsa R)."""
     macs = sum(_mont_macs(sk.lc, 0, -(-8 * a_bytes // sk.table_window) * (1 - 2.0 ** -sk.table_window))
                for sk in subs) + 2 * k.ln * k.ln + _mont_macs(k.lc, 0, 1)
     issued = sum(_mont_macs(sk.desc.n2_28_len if sk.desc.off_table28 >= 0 else sk.lc, 0,
@@ -405,7 +404,7 @@ def stage_p_crt(k, subs, a_bytes, N, t, t_public, t_setup):
     per_s = N / t
     return {"elements_per_s": round(per_s), "ms": round(t * 1e3, 3), "vs_public_path": round(t_public / t, 3),
             "macs_per_element": int(macs),
-            "method": "hs^a' mod p^2 and mod q^2 (W=%d/%d), CRT join, g(m) hsa mod n^2"
+            "method": "hs^a' R mod p^2 and mod q^2 (W=%d/%d), CRT join, mont(g(m), hsa R) mod n^2"
                       % (subs[0].table_window, subs[1].table_window),
             "roofline": {"bound": "valu", "achieved": round(per_s * macs / 1e12, 3),
                          "peak": round(MAD_U64_U32_PEAK / 1e12, 3), "unit": "TMAC/s",

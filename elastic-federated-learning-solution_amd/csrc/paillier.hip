@@ -154,9 +154,8 @@ __device__ __forceinline__ void fbpowm_mont(uint32_t (&acc)[LC], const Key& k, u
 // Encrypt (paillier.cc:103-131). hsa: [N][LC] normal-form limbs, or null -> fbpowm of a fresh a.
 template <int LN>
 __global__ __launch_bounds__(kPlBlock) void k_encrypt(Key k, const long long* __restrict__ m,
-                                                      const uint32_t* __restrict__ hsa,
-                                                      uint32_t* __restrict__ out, long long N,
-                                                      uint64_t seed, long long ctr0) {
+                                                      const uint32_t* hsa, uint32_t* out, long long N,
+                                                      uint64_t seed, long long ctr0, int hsa_mont) {
   constexpr int LC = 2 * LN;
   extern __shared__ uint32_t lds[];
   const int S = blockDim.x;
@@ -173,7 +172,7 @@ __global__ __launch_bounds__(kPlBlock) void k_encrypt(Key k, const long long* __
     make_g<LN>(c, m[i], n, n2);
     g_to_lds<LC>(bcol, S, hsa + i * LC);
     mont_mul<LC>(c, LdsCol{bcol, S}, n2, k.d.n2_minv);
-    mont_mul<LC>(c, Uniform{k.at(k.d.off_n2_r2)}, n2, k.d.n2_minv);
+    if (!hsa_mont) mont_mul<LC>(c, Uniform{k.at(k.d.off_n2_r2)}, n2, k.d.n2_minv);   // hsa_mont: hsa R given
   } else {
     draw_a(acol, S, (k.d.a_bits + 31) >> 5, k.d.a_bits, seed, (uint64_t)(ctr0 + i));
     fbpowm_mont<LC>(c, k, acol, bcol, S);      // hs^a' * R
@@ -1098,10 +1097,11 @@ hipError_t dispatch_ln(int ln, A... args) {
 template <int LN>
 struct RunEncrypt {
   static hipError_t run(Key k, const long long* m, const uint32_t* hsa, uint32_t* out, long long N,
-                        uint64_t seed, long long ctr0, hipStream_t s) {
+                        uint64_t seed, long long ctr0, hipStream_t s, int hsa_mont = 0) {
     const int aw = (k.d.a_bits + 31) / 32;
     const size_t lds = (size_t)((aw > 2 * LN ? aw : 2 * LN) + 2 * LN) * kPlBlock * 4;
-    hipLaunchKernelGGL((k_encrypt<LN>), dim3(grid_of(N)), dim3(kPlBlock), lds, s, k, m, hsa, out, N, seed, ctr0);
+    hipLaunchKernelGGL((k_encrypt<LN>), dim3(grid_of(N)), dim3(kPlBlock), lds, s, k, m, hsa, out, N, seed, ctr0,
+                       hsa_mont);
     return hipGetLastError();
   }
 };
@@ -1217,7 +1217,7 @@ EFL_API int efl_pl_fbpowm(const void* key_block, const efl_pl_key* key, const ui
 }
 
 EFL_API int efl_pl_crt_join(const void* key_block, const efl_pl_key* key, const uint32_t* xp, const uint32_t* xq,
-                            uint32_t* z, int64_t n, void* stream) {
+                            const int64_t* plaintext, uint32_t* z, int64_t n, void* stream) {
   if (!key_ok(key, true, 128)) return key && !key->has_private ? EFL_E_ABORTED : EFL_E_INVALID_ARGUMENT;
   if (n <= 0) return n < 0 ? EFL_E_INVALID_ARGUMENT : EFL_OK;
   Key k{(const uint32_t*)key_block, *key};
@@ -1230,7 +1230,15 @@ EFL_API int efl_pl_crt_join(const void* key_block, const efl_pl_key* key, const 
     case 64: hipLaunchKernelGGL((k_crt_join<64>), dim3(g), dim3(kPlBlock), lds, s, k, xp, xq, z, (long long)n); break;
     default: hipLaunchKernelGGL((k_crt_join<128>), dim3(g), dim3(kPlBlock), lds, s, k, xp, xq, z, (long long)n); break;
   }
-  return hip_status(hipGetLastError(), "efl_pl_crt_join");
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !plaintext) return hip_status(e, "efl_pl_crt_join");
+  // encryption: z holds hsa R mod n^2; g(m) hsa = mont(g, hsa R), one product, in place (each lane
+  // reads its element's words of z before it writes them)
+  const int C = slicing(key->ln, 0);
+  const long long* m = (const long long*)plaintext;
+  e = C ? pl::sl_encrypt(k, C, m, z, z, (long long)n, 0, 0, s, 1)
+        : dispatch_ln<RunEncrypt>(key->ln, k, m, (const uint32_t*)z, z, (long long)n, (uint64_t)0, 0ll, s, 1);
+  return hip_status(e, "efl_pl_crt_join");
 }
 
 EFL_API int efl_pl_decrypt(const void* key_block, const efl_pl_key* key, const uint32_t* ciphertext,

@@ -164,9 +164,8 @@ __device__ __forceinline__ void fbpowm_mont(uint32_t (&acc)[C], const Key& k, ui
 // ------------------------------------------------------------------------------------------
 template <int C, int G>
 __global__ __launch_bounds__(kSlBlock) SL_OCC void k_encrypt(Key k, const long long* __restrict__ m,
-                                                      const uint32_t* __restrict__ hsa,
-                                                      uint32_t* __restrict__ out, long long N, uint64_t seed,
-                                                      long long ctr0) {
+                                                      const uint32_t* hsa, uint32_t* out, long long N,
+                                                      uint64_t seed, long long ctr0, int hsa_mont) {
   constexpr int L = C * G, E = kSlBlock / G;
   extern __shared__ uint32_t lds[];
   SL_ELEMENT(E, G)
@@ -184,7 +183,8 @@ __global__ __launch_bounds__(kSlBlock) SL_OCC void k_encrypt(Key k, const long l
     make_g<C, G>(c, m[i], k, n2, g);
     lds_sync();
     mont_mul<C, G>(c, LdsElem{B, E}, n2, minv, g);
-    mont_mul<C, G>(c, Uniform{k.at(k.d.off_n2_r2)}, n2, minv, g);
+    // hsa_mont: hsa is hsa R mod n^2 (efl_pl_crt_join), so the one product above is g hsa
+    if (!hsa_mont) mont_mul<C, G>(c, Uniform{k.at(k.d.off_n2_r2)}, n2, minv, g);
   } else {
     draw_a<G>(A, E, words, k.d.a_bits, seed, (uint64_t)(ctr0 + i), g);
     lds_sync();
@@ -1255,10 +1255,10 @@ inline unsigned grid_of(long long N, int G) {
 
 template <int C, int G>
 hipError_t run_encrypt(const Key& k, const long long* m, const uint32_t* hsa, uint32_t* out, long long N,
-                       uint64_t seed, long long ctr0, hipStream_t s) {
+                       uint64_t seed, long long ctr0, hipStream_t s, int hsa_mont) {
   const int aw = (k.d.a_bits + 31) / 32;
   hipLaunchKernelGGL((k_encrypt<C, G>), dim3(grid_of(N, G)), dim3(kSlBlock), (size_t)(C * G + aw) * (kSlBlock / G) * 4, s, k, m,
-                     hsa, out, N, seed, ctr0);
+                     hsa, out, N, seed, ctr0, hsa_mont);
   return hipGetLastError();
 }
 template <int C, int G>
@@ -1455,11 +1455,11 @@ inline bool table28_for(const Key& k, int C) {
 }
 
 hipError_t sl_encrypt(const Key& k, int C, const long long* m, const uint32_t* hsa, uint32_t* out, long long N,
-                      uint64_t seed, long long ctr0, hipStream_t s) {
+                      uint64_t seed, long long ctr0, hipStream_t s, int hsa_mont) {
   if (!hsa && table28_for(k, C)) {
     SL_DISPATCH(2 * k.d.ln, C, (run_encrypt28<CC, GG>(k, m, out, N, seed, ctr0, s)))
   }
-  SL_DISPATCH(2 * k.d.ln, C, (run_encrypt<CC, GG>(k, m, hsa, out, N, seed, ctr0, s)))
+  SL_DISPATCH(2 * k.d.ln, C, (run_encrypt<CC, GG>(k, m, hsa, out, N, seed, ctr0, s, hsa_mont)))
 }
 hipError_t sl_fbpowm(const Key& k, int C, const uint32_t* a, uint32_t* out, long long N, uint64_t seed,
                      long long ctr0, hipStream_t s) {

@@ -162,7 +162,7 @@ struct ExpShift {
 // modulus the op works in (2*ln for n^2 ops, ln for decryption's p^2 / q^2).
 bool sliced_available(int L, int C);
 hipError_t sl_encrypt(const Key& k, int C, const long long* m, const uint32_t* hsa, uint32_t* out, long long N,
-                      uint64_t seed, long long ctr0, hipStream_t s);
+                      uint64_t seed, long long ctr0, hipStream_t s, int hsa_mont = 0);
 hipError_t sl_fbpowm(const Key& k, int C, const uint32_t* a, uint32_t* out, long long N, uint64_t seed,
                      long long ctr0, hipStream_t s);
 hipError_t sl_add(const Key& k, int C, const uint32_t* x, const uint32_t* y, uint32_t* out, long long N,

@@ -52,7 +52,7 @@ _PK = ctypes.POINTER(PlKey)
 for _name, _args in {
     "efl_pl_encrypt": [_vp, _PK, _vp, _vp, _vp, _i64, _u64, _i64, _vp],
     "efl_pl_fbpowm": [_vp, _PK, _vp, _vp, _i64, _u64, _i64, _vp],
-    "efl_pl_crt_join": [_vp, _PK, _vp, _vp, _vp, _i64, _vp],
+    "efl_pl_crt_join": [_vp, _PK, _vp, _vp, _vp, _vp, _i64, _vp],
     "efl_pl_decrypt": [_vp, _PK, _vp, _vp, _vp, _i64, _vp],
     "efl_pl_add": [_vp, _PK, _vp, _vp, _vp, _i64, _vp],
     "efl_pl_powm": [_vp, _PK, _vp, _vp, _i32, _vp, _i64, _vp],
@@ -408,12 +408,14 @@ class KeyBlock:
             if self.desc.has_private and os.environ.get("EFL_PL_CRT_ENCRYPT", "1") != "0":
                 subs = []
                 p2, q2 = self.p * self.p, self.q * self.q
-                for x, start in ((self.p, pow(q2, -1, p2)), (self.q, pow(p2, -1, q2))):
+                R = 1 << (32 * self.lc)   # the n^2 Montgomery radix: the join yields hsa R (efl_pl_crt_join)
+                for x, start in ((self.p, R * pow(q2, -1, p2)), (self.q, R * pow(p2, -1, q2))):
                     ln_x = next((c for c in _LIMB_CLASSES if 32 * c >= x.bit_length()), None)
                     if ln_x is None or 2 * ln_x != self.ln:
                         return None
-                    # the walk mod p^2 yields hs^(a') (q^2)^-1, mod q^2 hs^(a') (p^2)^-1: the join
-                    # z = q^2 yp + p^2 yq mod n^2 then needs no modular product
+                    # the walk mod p^2 yields hs^(a') R (q^2)^-1, mod q^2 hs^(a') R (p^2)^-1: the join
+                    # v = q^2 yp + p^2 yq mod n^2 = hs^(a') R then needs no modular product, and
+                    # g(m) hs^(a') = mont(g(m), v) is one
                     subs.append(KeyBlock(x, self.hs % (x * x), self.a_bits, self.group_size, device=self.device,
                                          walk_start=start))
                 self._crt = tuple(subs)
@@ -667,10 +669,10 @@ class PaillierKeypair(object):
         return CipherTensor(limbs, hx.shape, k)
 
     # -- ops -----------------------------------------------------------------------------
-    def _fresh_hsa(self, n, counter_base, a_dev=None):
-        """hs^(a') mod n^2 ([n, 2 ln] limbs) for the Philox draws at counters counter_base + i (or
-        the given exponents a_dev) by CRT, when this keypair holds the private key (KeyBlock.crt_keys);
-        None otherwise."""
+    def _crt_encrypt(self, m, n, counter_base, a_dev=None):
+        """The key owner's path (KeyBlock.crt_keys): ciphertexts of the int64 device tensor m ([n, 2 ln]
+        limbs) for the Philox draws at counters counter_base + i (or the given exponents a_dev) —
+        m = 0 gives hs^(a') itself. None when this keypair cannot take it."""
         k = self.key
         subs = k.crt_keys() if self.crt_encrypt else None
         if subs is None or n == 0:
@@ -683,7 +685,8 @@ class PaillierKeypair(object):
                                               x.data_ptr(), n, self.seed, counter_base, sh))
             parts.append(x)
         z = torch.empty((n, k.lc), dtype=torch.int32, device=k.device)
-        _efl_lib.check(_lib.efl_pl_crt_join(*k.args(), parts[0].data_ptr(), parts[1].data_ptr(), z.data_ptr(), n, sh))
+        _efl_lib.check(_lib.efl_pl_crt_join(*k.args(), parts[0].data_ptr(), parts[1].data_ptr(), m.data_ptr(),
+                                            z.data_ptr(), n, sh))
         return z
 
     def encrypt(self, plaintext, hsa=None, counter_base=None):
@@ -712,12 +715,13 @@ class PaillierKeypair(object):
         ctr = self.counter if counter_base is None else int(counter_base)
         if counter_base is None:
             self.counter += N
-        if hsa_limbs is None:
-            hsa_limbs = self._fresh_hsa(N, ctr)   # the key owner: hs^(a') by CRT, same bits
-            zero_idx = None
-        _efl_lib.check(_lib.efl_pl_encrypt(*k.args(), m.data_ptr(),
-                                           hsa_limbs.data_ptr() if hsa_limbs is not None else None,
-                                           out.data_ptr(), N, self.seed, ctr, _stream(k.device)))
+        crt = self._crt_encrypt(m, N, ctr) if hsa_limbs is None else None   # the key owner: by CRT, same bits
+        if crt is not None:
+            out = crt
+        else:
+            _efl_lib.check(_lib.efl_pl_encrypt(*k.args(), m.data_ptr(),
+                                               hsa_limbs.data_ptr() if hsa_limbs is not None else None,
+                                               out.data_ptr(), N, self.seed, ctr, _stream(k.device)))
         if hsa_limbs is not None and zero_idx is not None and zero_idx.size:
             # the rows whose hsa is "0" draw a fresh a at their own index's counter (ctr + idx),
             # inside this call's range: rows with a given hsa consume no counter
@@ -725,10 +729,12 @@ class PaillierKeypair(object):
             sub = torch.empty((idx.numel(), k.lc), dtype=torch.int32, device=k.device)
             msub = m[idx].contiguous()
             for j0, j1, c0 in _counter_runs(zero_idx):
-                h = self._fresh_hsa(j1 - j0, ctr + c0)
-                _efl_lib.check(_lib.efl_pl_encrypt(*k.args(), msub[j0:j1].data_ptr(), h.data_ptr() if h is not None else None,
-                                                   sub[j0:j1].data_ptr(), j1 - j0, self.seed, ctr + c0,
-                                                   _stream(k.device)))
+                h = self._crt_encrypt(msub[j0:j1], j1 - j0, ctr + c0)
+                if h is not None:
+                    sub[j0:j1] = h
+                    continue
+                _efl_lib.check(_lib.efl_pl_encrypt(*k.args(), msub[j0:j1].data_ptr(), None, sub[j0:j1].data_ptr(),
+                                                   j1 - j0, self.seed, ctr + c0, _stream(k.device)))
             out[idx] = sub
         return PaillierTensor(self, CipherTensor(out, shape, k))
 
@@ -751,7 +757,8 @@ class PaillierKeypair(object):
                 raise errors.InvalidArgumentError("exponent wider than the fixed-base table")
             arr = np.stack([_limbs(v, words) for v in a]) if n else np.zeros((0, words), "<u4")
             a_dev = torch.from_numpy(arr.view(np.int32)).to(k.device)
-        out = self._fresh_hsa(n, counter_base, a_dev if a is not None else None)
+        zeros = torch.zeros(n, dtype=torch.int64, device=k.device)   # g(0) = 1: the join gives hs^(a')
+        out = self._crt_encrypt(zeros, n, counter_base, a_dev if a is not None else None)
         if out is None:
             out = torch.empty((n, k.lc), dtype=torch.int32, device=k.device)
             _efl_lib.check(_lib.efl_pl_fbpowm(*k.args(), a_dev.data_ptr() if a is not None else None,

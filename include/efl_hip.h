@@ -213,14 +213,17 @@ int efl_pl_encrypt(const void* key_block, const efl_pl_key* key, const int64_t* 
 int efl_pl_fbpowm(const void* key_block, const efl_pl_key* key, const uint32_t* a, uint32_t* hsa,
                   int64_t n, uint64_t seed, int64_t counter_base, void* stream);
 
-/* The key owner's fixed-base exponentiation by CRT (no reference counterpart: the reference's
- * Encrypt, paillier.cc:103-131, always works mod n^2). z[i] ([n][2*ln] limbs) = q^2 yp[i] + p^2
- * yq[i] mod n^2 for yp[i] < p^2, yq[i] < q^2 ([n][ln] limbs each). With yp = x (q^2)^-1 mod p^2 and
- * yq = x (p^2)^-1 mod q^2, z = x mod n^2: the efl package gets them from efl_pl_fbpowm under the
- * keys (p, hs mod p^2) and (q, hs mod q^2) whose walks start from (q^2)^-1 and (p^2)^-1, so z is
- * hs^(a') mod n^2, bit for bit, from half-length products. ABORTED without the private key. */
-int efl_pl_crt_join(const void* key_block, const efl_pl_key* key, const uint32_t* xp, const uint32_t* xq,
-                    uint32_t* z, int64_t n, void* stream);
+/* The key owner's fixed-base exponentiation and encryption by CRT (no reference counterpart: the
+ * reference's Encrypt, paillier.cc:103-131, always works mod n^2). v[i] = q^2 yp[i] + p^2 yq[i] mod
+ * n^2 for yp[i] < p^2, yq[i] < q^2 ([n][ln] limbs each); with yp = x (q^2)^-1 mod p^2 and yq = x
+ * (p^2)^-1 mod q^2, v = x mod n^2. plaintext NULL: z[i] = v[i] ([n][2*ln] limbs). plaintext given
+ * (int64 m): v is taken as hsa R mod n^2 (R = 2^(64*ln), the n^2 Montgomery radix) and z[i] =
+ * (1 + |m| n)^(sign) hsa mod n^2, the PaillierEncrypt ciphertext, with one Montgomery product. The
+ * efl package gets yp and yq from efl_pl_fbpowm under the keys (p, hs mod p^2) and (q, hs mod q^2)
+ * whose walks start from R (q^2)^-1 and R (p^2)^-1: the same ciphertexts, bit for bit, from
+ * half-length products. ABORTED without the private key. */
+int efl_pl_crt_join(const void* key_block, const efl_pl_key* key, const uint32_t* yp, const uint32_t* yq,
+                    const int64_t* plaintext, uint32_t* z, int64_t n, void* stream);
 
 /*
  * PaillierDecrypt (paillier.cc:505-561, _Decrypt :296-312): CRT decryption of [n][2*ln]

@@ -61,7 +61,7 @@ def test_crt_join(efl, k):
     yq = [0, 1, q2 - 1, q2 - 1, 0, 7, 1] + [rng.randrange(q2) for _ in range(250)]
     z = torch.empty((len(yp), key.lc), dtype=torch.int32, device="cuda")
     Yp, Yq = limbs(yp, key.ln), limbs(yq, key.ln)
-    rc = pc._lib.efl_pl_crt_join(*key.args(), Yp.data_ptr(), Yq.data_ptr(), z.data_ptr(), len(yp),
+    rc = pc._lib.efl_pl_crt_join(*key.args(), Yp.data_ptr(), Yq.data_ptr(), None, z.data_ptr(), len(yp),
                                  torch.cuda.current_stream().cuda_stream)
     assert rc == 0
     got = ints(z)
@@ -76,8 +76,21 @@ def test_crt_join(efl, k):
     ip, iq = pow(q2, -1, p2), pow(p2, -1, q2)
     Yp, Yq = limbs([x % p2 * ip % p2 for x in xs], key.ln), limbs([x % q2 * iq % q2 for x in xs], key.ln)
     z = torch.empty((len(xs), key.lc), dtype=torch.int32, device="cuda")
-    assert pc._lib.efl_pl_crt_join(*key.args(), Yp.data_ptr(), Yq.data_ptr(), z.data_ptr(), len(xs), None) == 0
+    assert pc._lib.efl_pl_crt_join(*key.args(), Yp.data_ptr(), Yq.data_ptr(), None, z.data_ptr(), len(xs), None) == 0
     assert ints(z) == xs
+    # with the plaintext: v is hsa R, z = (1 + |m| n)^(sign) hsa mod n^2 (in place of z's own words)
+    R = 1 << (32 * key.lc)
+    ms = [rng.randrange(-2**63, 2**63) for _ in xs]
+    ms[:4] = [0, -1, 2**63 - 1, -2**63]
+    m = torch.tensor(ms, dtype=torch.int64, device="cuda")
+    assert pc._lib.efl_pl_crt_join(*key.args(), Yp.data_ptr(), Yq.data_ptr(), m.data_ptr(), z.data_ptr(), len(xs),
+                                   None) == 0
+    Rinv = pow(R, -1, n2)
+    for x, mi, got in zip(xs, ms, ints(z)):
+        gm = (1 + abs(mi) * key.n) % n2
+        if mi < 0:
+            gm = pow(gm, -1, n2)
+        assert got == gm * x * Rinv % n2
 
 
 @pytest.mark.parametrize("k", CRT_KEYS, ids=ids)
@@ -105,6 +118,25 @@ def test_crt_encrypt_equals_public_path(efl, k):
     okp = P.Keypair(int(k["n"], 16), int(k["hs"], 16), k["a_bits"] // 8, g)
     for i in (0, 123, 299):
         assert f1[i] == P.hx(P.fbpowm(okp.hs, okp.n2, philox.draw_a(77, 3 + i, k["a_bits"]), g))
+
+
+@pytest.mark.parametrize("c", [0, 8, 16, 32])
+def test_crt_encrypt_every_family(efl, c):
+    """The join's g(m) product runs the main key's encryption kernel with hsa in Montgomery form:
+    every kernel family of the 1024-bit key (one lane, sliced C = 8 / 16 / 32) gives the n^2 path's
+    ciphertexts."""
+    from efl.privacy import paillier_cipher as pc
+    k = CRT_KEYS[0]
+    ln = k["n_bytes"] // 4
+    m = torch.tensor([0, 1, -1, 2**63 - 1, -2**63] + list(range(-60, 60, 7)), dtype=torch.int64)
+    prev = pc.set_kernel_slicing(ln, False, c)
+    try:
+        kp = keypair(efl, k, seed=5)
+        crt = kp.encrypt(m, counter_base=9).tensor.to_hex().strings()
+        kp.crt_encrypt = False
+        assert kp.encrypt(m, counter_base=9).tensor.to_hex().strings() == crt
+    finally:
+        pc.set_kernel_slicing(ln, False, prev)
 
 
 def test_crt_mixed_hsa_rows(efl):
@@ -143,5 +175,5 @@ def test_crt_join_errors(efl):
     from efl.privacy import paillier_cipher as pc
     kp = keypair(efl, CRT_KEYS[0], private=False)
     z = torch.empty((1, kp.key.lc), dtype=torch.int32, device="cuda")
-    rc = pc._lib.efl_pl_crt_join(*kp.key.args(), z.data_ptr(), z.data_ptr(), z.data_ptr(), 1, None)
+    rc = pc._lib.efl_pl_crt_join(*kp.key.args(), z.data_ptr(), z.data_ptr(), None, z.data_ptr(), 1, None)
     assert rc != 0

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """The key owner's CRT encryption, kernel by kernel (for rocprofv3 --kernel-trace --stats): for each
-Stage-P key, REPS rounds of [sub fbpowm p, sub fbpowm q, efl_pl_crt_join, efl_pl_encrypt with hsa]
-beside the public-key efl_pl_encrypt, same draws. Prints per-leg HIP-event times as JSON lines.
+Stage-P key, REPS rounds of [sub fbpowm p, sub fbpowm q, efl_pl_crt_join without and with m]
+beside the public-key efl_pl_encrypt, same draws (join alone, and join + g(m) product). Prints per-leg HIP-event times as JSON lines.
 
     python tools/crt_probe.py [--reps 5]
 """
@@ -45,8 +45,9 @@ def main():
             "public": lambda: lib.efl_pl_encrypt(*k.args(), m.data_ptr(), None, ct.data_ptr(), N, 7, 0, sh),
             "fbpowm_p": lambda: lib.efl_pl_fbpowm(*subs[0].args(), None, xs[0].data_ptr(), N, 7, 0, sh),
             "fbpowm_q": lambda: lib.efl_pl_fbpowm(*subs[1].args(), None, xs[1].data_ptr(), N, 7, 0, sh),
-            "join": lambda: lib.efl_pl_crt_join(*k.args(), xs[0].data_ptr(), xs[1].data_ptr(), hsa.data_ptr(), N, sh),
-            "encrypt_hsa": lambda: lib.efl_pl_encrypt(*k.args(), m.data_ptr(), hsa.data_ptr(), ct2.data_ptr(), N, 7, 0, sh),
+            "join": lambda: lib.efl_pl_crt_join(*k.args(), xs[0].data_ptr(), xs[1].data_ptr(), None, hsa.data_ptr(), N, sh),
+            "join_encrypt": lambda: lib.efl_pl_crt_join(*k.args(), xs[0].data_ptr(), xs[1].data_ptr(), m.data_ptr(),
+                                                        ct2.data_ptr(), N, sh),
         }
         out = {"key": label, "elements": N, "ms": {}}
         for name, fn in legs.items():
