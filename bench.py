@@ -74,7 +74,7 @@ def usable_cores():
     return aff, f"sched_getaffinity: {aff} CPUs" + (f" (cgroup quota {quota:g})" if quota else "")
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
@@ -91,7 +91,7 @@ def parse():
     p.add_argument("--rows", type=int, default=ROWS)
     p.add_argument("--stage", choices=("f", "p"), default="f",
                    help="f: the BASELINE.json metric (fixed-point codec); p: the Paillier report")
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
 def broadcast_seed(world, rank):
@@ -616,12 +616,63 @@ def config5(timeout_s=240):
         return {"error": repr(e)[:300]}
 
 
-def main():
-    args = parse()
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args, argv):
+    """`bench.py --gpus N` run without a torchrun environment: start the N ranks as children
+    (torch.distributed.run, one process per GPU, rendezvous on 127.0.0.1) and relay rank 0's JSON
+    line. This process never touches the GPU (torch.cuda.device_count() does not initialise it on
+    this image) and never execs: the children are fresh processes. Exit status: the children's, or
+    3 when the world that ran is not the one asked for."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + argv
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    line = None
+    for ln in proc.stdout:                     # progress lines pass through; the JSON line is held
+        if ln.startswith("{") and '"metric"' in ln:
+            line = ln.strip()
+        else:
+            sys.stderr.write(ln)
+            sys.stderr.flush()
+    rc = proc.wait()
+    if rc:
+        return rc
+    if line is None:
+        print("bench: rank 0 printed no result line", file=sys.stderr)
+        return 3
+    out = json.loads(line)
+    out["launcher"] = f"bench.py --gpus {args.gpus}: torch.distributed.run children, rendezvous 127.0.0.1"
+    print(json.dumps(out), flush=True)
+    if out.get("n_gpus") != args.gpus:
+        print(f"bench: asked for {args.gpus} ranks, {out.get('n_gpus')} ran", file=sys.stderr)
+        return 3
+    return 0
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
     if args.stage == "p":
         if args.cpu_threads is None:
             args.cpu_threads = usable_cores()[0]
         return stage_p(args)
+    if args.gpus < 1:
+        raise SystemExit("bench: --gpus must be >= 1")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        return launch_ranks(args, argv)
+    if int(env_world or 1) != args.gpus:
+        # checked before any GPU or process-group call: a run labelled N must be N ranks
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={env_world}", file=sys.stderr)
+        return 3
     from efl import distributed as edist
     world, rank, local, dev_index, backend = edist.init_from_env(args.backend)
     import efl
@@ -768,4 +819,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

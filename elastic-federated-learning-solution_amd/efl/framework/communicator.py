@@ -33,6 +33,7 @@ import os
 import threading
 import time
 import warnings
+import zlib
 from concurrent import futures
 
 import grpc
@@ -59,6 +60,22 @@ _DT_OF_TORCH = {v: k for k, v in _TORCH_OF_DT.items()}
 def _env_int(name, default):
     v = os.environ.get(name, "")
     return int(v) if v else default
+
+
+_PAIR_SUFFIXES = ("_mantissa", "_exponent")
+
+
+def channel_of(name: str, nchan: int) -> int:
+    """The client connection a message name always travels on: a stable hash of the name, so two
+    sends of one name keep their order (the receiver parks each name's messages FIFO). A hook's
+    '<x>_mantissa' / '<x>_exponent' pair hashes '<x>' and takes adjacent channels, so the two large
+    payloads of one send still cross on two connections at once."""
+    if nchan <= 1:
+        return 0
+    for i, suf in enumerate(_PAIR_SUFFIXES):
+        if name.endswith(suf):
+            return (zlib.crc32(name[:-len(suf)].encode()) + i) % nchan
+    return zlib.crc32(name.encode()) % nchan
 
 
 def _http2_opts():
@@ -312,7 +329,7 @@ class Communicator(object):
         self._channel = self._channels[0]
         self._send_rpcs = [ch.unary_unary(_SEND) for ch in self._channels]
         self._send_rpc = self._send_rpcs[0]
-        self._next_chan = 0
+        self._inflight = {}
 
     # server side ---------------------------------------------------------------------
     def _on_connect(self, request, context):
@@ -364,13 +381,45 @@ class Communicator(object):
             shape = tuple(t.shape)
             content = t.view(torch.uint8).numpy().reshape(-1) if t.numel() else b""
         req = wire.message_request(name, self.step, dtype, shape, content)
-        # messages round-robin over the channels: two large payloads sent back to back (a hook's
-        # mantissa and exponent) travel on two connections at once
+        return SendHandle([(name, self._send_ordered(name, req))])
+
+    def _send_ordered(self, name, req):
+        """Issue the SendMessage RPC for `name`, after the previous send of the same name completed
+        if one is still in flight. Concurrent unary RPCs are not ordered on the server (a small
+        message overtakes a large one even on one connection), and the receiver hands a name's
+        parked messages over FIFO; the reference keeps one in-flight message per name at all
+        (communication_service.cc:236-238 replaces the parked call). A send completes when the peer
+        has received it, so chaining costs nothing unless one name is sent twice before the first
+        is consumed."""
+        rpc = self._send_rpcs[channel_of(name, len(self._send_rpcs))]
+        timeout = self._timeout
         with self._lock:
-            rpc = self._send_rpcs[self._next_chan]
-            self._next_chan = (self._next_chan + 1) % len(self._send_rpcs)
-        fut = rpc.future(req, timeout=self._timeout)
-        return SendHandle([(name, fut)])
+            prev = self._inflight.get(name)
+            if prev is None or prev.done():
+                fut = rpc.future(req, timeout=timeout)
+            else:
+                fut = futures.Future()
+
+                def relay(g):
+                    e = g.exception()
+                    if e is not None:
+                        fut.set_exception(e)
+                    else:
+                        fut.set_result(g.result())
+
+                def start(_):
+                    try:
+                        rpc.future(req, timeout=timeout).add_done_callback(relay)
+                    except Exception as e:       # noqa: BLE001 - surfaced by SendHandle.result
+                        fut.set_exception(e)
+                prev.add_done_callback(start)
+            self._inflight[name] = fut
+
+        def forget(_):
+            if self._inflight.get(name) is fut:
+                self._inflight.pop(name, None)
+        fut.add_done_callback(forget)
+        return fut
 
     def _take(self, name, step):
         """Pop the parked message for (name, step) or register a waiter; called under the lock."""

@@ -247,6 +247,10 @@ class KeyBlock:
         so efl_pl_fbpowm gives walk_start * hs^(a') mod n^2 (the CRT keys of crt_keys)."""
         if n.bit_length() < 128:
             raise errors.UnimplementedError("n of fewer than 128 bits is not supported on the GPU")
+        if p is not None and q is not None and p == q:
+            # q^-1 mod p does not exist: the reference's mpz_invert fails silently there and its
+            # decryption is wrong (paillier.cc:88-99); refuse the key instead
+            raise errors.InvalidArgumentError("private key: p and q must be distinct")
         if p is not None and q is not None and q >= 2 * p:
             p, q = q, p        # CRT below reduces mq mod p with one subtraction: needs q < 2p
         self.n, self.hs, self.p, self.q = n, hs, p, q
@@ -402,10 +406,13 @@ class KeyBlock:
         half-length moduli (a quarter of the limb products each) and one CRT join
         (efl_pl_crt_join): the same value, bit for bit, as the public-key path. None without the
         private key, with EFL_PL_CRT_ENCRYPT=0, or when p and q are not half-length primes of a
-        supported limb class (512-bit n: 256-bit primes)."""
+        supported limb class (512-bit n: 256-bit primes). Also None when the private key does not
+        factor n (p q != n, or p == q): the reference's Encrypt works mod n^2 only, so such a key
+        still encrypts correctly there (paillier.cc:103-131), and the public-key path keeps that."""
         if self._crt is None:
             self._crt = False
-            if self.desc.has_private and os.environ.get("EFL_PL_CRT_ENCRYPT", "1") != "0":
+            if self.desc.has_private and os.environ.get("EFL_PL_CRT_ENCRYPT", "1") != "0" \
+                    and self.p != self.q and self.p * self.q == self.n:
                 subs = []
                 p2, q2 = self.p * self.p, self.q * self.q
                 R = 1 << (32 * self.lc)   # the n^2 Montgomery radix: the join yields hsa R (efl_pl_crt_join)

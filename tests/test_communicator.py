@@ -82,6 +82,32 @@ def test_readonly_raw_recv_is_a_view(comms):
     assert torch.equal(view, m) and torch.equal(copy, m)
 
 
+def test_channel_of_is_stable_and_splits_pairs():
+    from efl.framework.communicator import channel_of
+    for n in ("act", "grad/0", "x_mantissa", "emb"):
+        assert channel_of(n, 2) == channel_of(n, 2) and channel_of(n, 1) == 0
+    for base in ("act", "dense_1/out", "y"):
+        a, b = channel_of(base + "_mantissa", 2), channel_of(base + "_exponent", 2)
+        assert {a, b} == {0, 1}
+
+
+def test_same_name_back_to_back_keeps_order():
+    """Several sends of one name in one step, over two connections: the receiver gets them in send
+    order (one name always travels on one channel)."""
+    leader, follower = pair(default_timeout_milliseconds=5000, channels=2)
+    try:
+        big = [torch.full((1 << 20,), float(i)) for i in range(4)]
+        hs = [follower.send("dup", t) for t in (big[0], torch.ones(3), big[1], torch.full((5,), 2.0))]
+        got = [leader.recv("dup") for _ in range(4)]
+        for h in hs:
+            h.result(timeout=5)
+        assert torch.equal(got[0], big[0]) and torch.equal(got[1], torch.ones(3))
+        assert torch.equal(got[2], big[1]) and torch.equal(got[3], torch.full((5,), 2.0))
+    finally:
+        leader.shutdown()
+        follower.shutdown()
+
+
 def test_send_completes_only_after_peer_recv(comms):
     leader, follower = comms
     h = follower.send("late", torch.ones(3))

@@ -13,6 +13,7 @@ What is checked (in the parent, against float64 arithmetic of the same protocol)
   * neither share alone is the model: the sender's share is non-zero and masked.
 Dense and Weight layers both."""
 import multiprocessing as mp
+import weakref
 
 import numpy as np
 import pytest
@@ -80,12 +81,105 @@ def party(role, kind, my, peer, q):
         q.put((role, None, traceback.format_exc()[-3000:]))
 
 
-def run_parties(kind):
+ROT_STEPS, ROT_INTERVAL = 5, 2
+
+
+def party_rotation(role, kind, my, peer, q):
+    """Five dense steps with create_keypair(..., update_step_interval=2): the sender generates a new
+    keypair before steps 0, 2 and 4 (PaillierHook.before_run, paillier.py:195-202) and the receiver
+    installs it. Records per step: the key's n, device memory around the re-key, the layer values."""
+    try:
+        import efl
+        Role = efl.privacy.Role
+        g = torch.Generator().manual_seed(12)
+        units = 4
+        xs = [torch.randn(B, F, generator=g) for _ in range(ROT_STEPS)]
+        t = torch.randn(B, units, generator=g)
+        c = efl.Communicator(role, 0, 1, f"127.0.0.1:{peer}", f"127.0.0.1:{my}",
+                             default_timeout_milliseconds=120000, connect_retry_seconds=0.1)
+        model = efl.FederalModel(c)
+        sender = role == "follower"
+        kp = model.create_keypair("kp", Role.SENDER if sender else Role.RECEIVER, update_step_interval=ROT_INTERVAL,
+                                  n_bytes=128, seed=7)
+        model.initialize()
+        rec = []
+        for step in range(ROT_STEPS):
+            torch.cuda.synchronize()
+            m0 = torch.cuda.memory_allocated()
+            old = weakref.ref(kp.key) if step else None
+            model.begin_step()                        # re-key on steps 0, 2, 4
+            torch.cuda.synchronize()
+            m1 = torch.cuda.memory_allocated()
+            key_bytes = kp.key.block.numel() * 4
+            rekeyed = old is not None and old() is not kp.key
+            old_alive = rekeyed and old() is not None
+            if sender:
+                out = model.paillier_sender_dense(xs[step].cuda(), "kp", "l1", LR, units, seed=1)
+                (w, lr), = model.paillier_vars_and_lrs()
+                before = w.detach().cpu().clone()
+                model.minimize(None)
+                vals = (before, w.detach().cpu().clone(), out.detach().cpu())
+            else:
+                y = model.paillier_recver_dense(None, "kp", "l1", LR, units, (B, F), seed=2)
+                (W, lr), = model.paillier_vars_and_lrs()
+                before = W.detach().cpu().clone()
+                loss = 0.5 * ((y - t.cuda()) ** 2).sum()
+                dy = (y - t.cuda()).detach()
+                model.minimize(None, loss)
+                vals = (before, W.detach().cpu().clone(), y.detach().cpu(), dy.cpu())
+                del y, loss, dy
+            subs = kp.key.crt_keys() if sender else None
+            crt_bytes = sum(s.block.numel() * 4 for s in subs) if subs else 0
+            model.end_step()
+            rec.append(dict(n=kp.key.n, m0=m0, m1=m1, key_bytes=key_bytes, crt_bytes=crt_bytes, rekeyed=rekeyed,
+                            old_alive=old_alive,
+                            vals=tuple(a.numpy() for a in vals)))
+        c.shutdown()
+        q.put((role, rec, None))
+    except BaseException:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((role, None, traceback.format_exc()[-3000:]))
+
+
+def test_key_rotation_every_two_steps():
+    """update_step_interval = 2 over five steps: both parties hold the same n on every step, n
+    changes exactly on steps 2 and 4, the layer's values stay right across each switch, and device
+    memory after a re-key is back at its level after the previous re-key (the old key block, its
+    fixed-base table and the key owner's CRT sub-tables are released)."""
+    res = run_parties("dense", target=party_rotation)
+    recv, send = res["leader"], res["follower"]
+    ns = [r["n"] for r in send]
+    assert ns == [r["n"] for r in recv]
+    assert ns[0] == ns[1] != ns[2] == ns[3] != ns[4] and ns[0] != ns[4]
+    assert [r["rekeyed"] for r in send] == [False, False, True, False, True]
+    assert [r["rekeyed"] for r in recv] == [False, False, True, False, True]
+    assert not any(r["old_alive"] for r in send + recv)      # nothing holds the replaced KeyBlock
+    g = torch.Generator().manual_seed(12)
+    xs = [torch.randn(B, F, generator=g).numpy().astype(np.float64) for _ in range(ROT_STEPS)]
+    for step in range(ROT_STEPS):
+        W0, W1, y, dy = (a.astype(np.float64) for a in recv[step]["vals"])
+        w0, w1, out = (a.astype(np.float64) for a in send[step]["vals"])
+        x = xs[step]
+        assert np.allclose(y, x @ qdp(W0) + x @ w0, rtol=1e-4, atol=1e-4), step
+        assert np.allclose((W1 + w1) - (W0 + w0), -LR * x.T @ qdp(dy), rtol=1e-4, atol=2e-5), step
+    for side in (send, recv):
+        key_bytes = side[2]["key_bytes"]
+        assert key_bytes > 1 << 20                       # the fixed-base table dominates (MiB scale)
+        # right after the re-keys of steps 2 and 4 the same bytes are live: nothing of the old key
+        # stays behind (a leak would add at least one key block)
+        assert abs(side[4]["m1"] - side[2]["m1"]) < key_bytes // 4, [r["m1"] for r in side]
+        # at the start of steps 3 and 4 (before the second re-key) as at step 2: steady state
+        assert abs(side[4]["m0"] - side[2]["m0"]) < key_bytes // 4, [r["m0"] for r in side]
+    # the key owner's CRT sub-tables are rebuilt for each new key and the old ones released
+    assert send[2]["crt_bytes"] > 0 and send[4]["crt_bytes"] == send[2]["crt_bytes"]
+
+
+def run_parties(kind, target=party):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     pl, pf = free_port(), free_port()
-    procs = [ctx.Process(target=party, args=("leader", kind, pl, pf, q)),
-             ctx.Process(target=party, args=("follower", kind, pf, pl, q))]
+    procs = [ctx.Process(target=target, args=("leader", kind, pl, pf, q)),
+             ctx.Process(target=target, args=("follower", kind, pf, pl, q))]
     for p in procs:
         p.start()
     results = {}

@@ -163,6 +163,26 @@ def test_crt_not_used_without_private_key_or_class(efl, monkeypatch):
     assert keypair(efl, CRT_KEYS[0]).key.crt_keys() is None
 
 
+def test_crt_not_used_for_private_key_not_factoring_n(efl):
+    """A private key whose p q != n: the reference's Encrypt (mod n^2 only) still gives valid
+    ciphertexts of n, so the key owner's encryption must take the public-key path, not the CRT
+    join (which would be wrong mod n^2)."""
+    from efl import errors
+    from efl.privacy import paillier_cipher as pc
+    k = CRT_KEYS[0]
+    _, _, p2, q2 = pc.generate_keypair_ints(k["n_bytes"], 24, random.Random(99))
+    kp = efl.paillier.Keypair(seed=8)
+    kp.set_keys_ints(int(k["n"], 16), int(k["hs"], 16), k["a_bits"] // 8, 1, p2, q2)
+    assert kp.key.crt_keys() is None
+    m = torch.tensor([0, 5, -7, 2**62, -2**63], dtype=torch.int64)
+    got = kp.encrypt(m, counter_base=3).tensor.to_hex().strings()
+    pub = keypair(efl, k, g=1, seed=8, private=False)
+    assert got == pub.encrypt(m, counter_base=3).tensor.to_hex().strings()
+    with pytest.raises(errors.InvalidArgumentError):
+        efl.paillier.Keypair(seed=1).set_keys_ints(int(k["n"], 16), int(k["hs"], 16), k["a_bits"] // 8, 1,
+                                                   p2, p2)
+
+
 def test_crt_keys_survive_set_private_key(efl):
     k = CRT_KEYS[0]
     kp = keypair(efl, k)

@@ -377,14 +377,16 @@ def _invert_and_negative_scalars(efl, k, kp):
         kp.invert(efl.HexTensor.from_ints([okp.n]))         # gcd(n, n^2) != 1
 
 
-@pytest.mark.parametrize("c", [0, 16])
-def test_matmul_vs_oracle(efl, c):
-    with family(16, False, c):
-        _matmul_vs_oracle(efl)
+@pytest.mark.parametrize("k,c", fams(ALL))
+def test_matmul_vs_oracle(efl, k, c):
+    """PaillierMatmul against the oracle bit for bit at every key size and n^2 kernel family (the
+    2048- and 4096-bit keys run k_matmul28 / k_mmevents at G = 2 / 4 lanes per number)."""
+    with family(k["n_bytes"] // 4, False, c):
+        _matmul_vs_oracle(efl, k)
 
 
-def _matmul_vs_oracle(efl):
-    k = ENC_KEYS[0]
+def _matmul_vs_oracle(efl, k=None):
+    k = k or ENC_KEYS[0]
     kp = keypair(efl, k)
     okp = P.Keypair(int(k["n"], 16), int(k["hs"], 16), k["a_bits"] // 8, 1, int(k["p"], 16), int(k["q"], 16))
     rng = np.random.default_rng(5)
@@ -397,7 +399,7 @@ def _matmul_vs_oracle(efl):
     ye = rng.integers(-25, -12, (v, w))
     zm, ze = kp.matmul(ct.tensor, torch.from_numpy(xe), torch.from_numpy(ym), torch.from_numpy(ye))
     xs = [[int(s, 16) for s in row] for row in np.array(ct.tensor.to_hex().strings()).reshape(u, v)]
-    om, oe = P.matmul(okp, xs, xe.tolist(), ym.tolist(), ye.tolist())
+    om, oe = _oracle_matmul(okp, xs, xe, ym, ye)
     assert np.array_equal(ze.cpu().numpy(), np.array(oe))
     assert zm.to_hex().to_ints() == [c for row in om for c in row]
     # and the plaintext meaning: sum_j xm*ym*2^(xe+ye-min)
@@ -407,8 +409,20 @@ def _matmul_vs_oracle(efl):
     assert dec == want
 
 
-def _matmul_case(efl, xe, ym, ye, seed):
-    k = ENC_KEYS[0]
+_ORACLE_MM = {}
+
+
+def _oracle_matmul(okp, xs, xe, ym, ye):
+    """oracle.paillier.matmul, memoised on its inputs: the result does not depend on the kernel
+    family, and a 4096-bit case costs the Python oracle up to ~10 s."""
+    key = (okp.n, str(xs), xe.tobytes(), ym.tobytes(), ye.tobytes())
+    if key not in _ORACLE_MM:
+        _ORACLE_MM[key] = P.matmul(okp, xs, xe.tolist(), ym.tolist(), ye.tolist())
+    return _ORACLE_MM[key]
+
+
+def _matmul_case(efl, xe, ym, ye, seed, k=None):
+    k = k or ENC_KEYS[0]
     kp = keypair(efl, k)
     okp = P.Keypair(int(k["n"], 16), int(k["hs"], 16), k["a_bits"] // 8, 1, int(k["p"], 16), int(k["q"], 16))
     u, v = xe.shape
@@ -416,20 +430,12 @@ def _matmul_case(efl, xe, ym, ye, seed):
     ct = kp.encrypt(torch.from_numpy(xm_plain))
     zm, ze = kp.matmul(ct.tensor, torch.from_numpy(xe), torch.from_numpy(ym), torch.from_numpy(ye))
     xs = [[int(s, 16) for s in row] for row in np.array(ct.tensor.to_hex().strings()).reshape(u, v)]
-    om, oe = P.matmul(okp, xs, xe.tolist(), ym.tolist(), ye.tolist())
+    om, oe = _oracle_matmul(okp, xs, xe, ym, ye)
     assert np.array_equal(ze.cpu().numpy(), np.array(oe))
     assert zm.to_hex().to_ints() == [c for row in om for c in row]
 
 
-@pytest.mark.parametrize("case", ["sorted", "level_scan", "over_capacity", "deep", "mixed"])
-@pytest.mark.parametrize("splits", [0, 1])
-@pytest.mark.parametrize("c", [16, 32])
-def test_matmul_schedule_paths(efl, case, splits, c):
-    """Every path of the multiply schedules (k_mmevents / k_matmul28) equals the oracle: the LDS
-    counting sort (levels < 128), the builder's level-major scan (levels 128..1023), and the
-    in-kernel scan for lists that do not fit — more than 5 windows per term (60-bit weights) or a
-    level past 1023 — alone and next to listed outputs in the same wave ("mixed": one row's
-    exponents spread past 1023)."""
+def _schedule_case(case):
     rng = np.random.default_rng(21)
     u, v, w = 3, 5, 4
     xe = rng.integers(-30, -10, (u, v))
@@ -444,6 +450,19 @@ def test_matmul_schedule_paths(efl, case, splits, c):
     elif case == "mixed":
         xe[1, 2] -= 1100
         ym[:, 1] = rng.integers(-2**60, 2**60, v)
+    return xe, ym, ye
+
+
+@pytest.mark.parametrize("case", ["sorted", "level_scan", "over_capacity", "deep", "mixed"])
+@pytest.mark.parametrize("splits", [0, 1])
+@pytest.mark.parametrize("c", [16, 32])
+def test_matmul_schedule_paths(efl, case, splits, c):
+    """Every path of the multiply schedules (k_mmevents / k_matmul28) equals the oracle: the LDS
+    counting sort (levels < 128), the builder's level-major scan (levels 128..1023), and the
+    in-kernel scan for lists that do not fit — more than 5 windows per term (60-bit weights) or a
+    level past 1023 — alone and next to listed outputs in the same wave ("mixed": one row's
+    exponents spread past 1023)."""
+    xe, ym, ye = _schedule_case(case)
     lib = efl.lib.raw()
     ln = ENC_KEYS[0]["n_bytes"] // 4
     prev = lib.efl_pl_tune(ln, 3, splits)
@@ -452,6 +471,16 @@ def test_matmul_schedule_paths(efl, case, splits, c):
             _matmul_case(efl, xe, ym, ye, 3)
     finally:
         lib.efl_pl_tune(ln, 3, prev)
+
+
+@pytest.mark.parametrize("case", ["sorted", "level_scan", "over_capacity", "deep", "mixed"])
+@pytest.mark.parametrize("k,c", fams(ALL[1:]))
+def test_matmul_schedule_paths_every_key(efl, k, c, case):
+    """The same schedule paths at the 1024-, 2048- and 4096-bit keys, every n^2 family, default
+    term splits: bit-identical to the oracle."""
+    xe, ym, ye = _schedule_case(case)
+    with family(k["n_bytes"] // 4, False, c):
+        _matmul_case(efl, xe, ym, ye, 3, k)
 
 
 @pytest.mark.parametrize("splits", [1, 2, 3, 4, 16])
