@@ -273,8 +273,16 @@ def _decode_hex(hx, exponent, dtype, flags):
     return back(y, home)
 
 
-def _ptr_table(ts, dev):
-    return torch.tensor([t.data_ptr() for t in ts], dtype=torch.int64).to(dev)
+def _carve(like, dtype, dev):
+    """Outputs of a batched op as views of one buffer, in batch order and 16-byte aligned, so
+    that adjacent inputs (slices of one table) make one run with them (coalesce_runs)."""
+    q = max(1, 16 // torch.empty((), dtype=dtype).element_size())
+    offs, total = [], 0
+    for t in like:
+        offs.append(total)
+        total += -(-t.numel() // q) * q
+    buf = torch.empty(total, dtype=dtype, device=dev)
+    return [buf[o:o + t.numel()].view(t.shape) for o, t in zip(offs, like)]
 
 
 def convert_to_fixed_point_batched(tensors, decrease_precision=None):
@@ -289,25 +297,67 @@ def convert_to_fixed_point_batched(tensors, decrease_precision=None):
     xs = [t.contiguous() for t in tensors]
     if any(t.dtype != xs[0].dtype or t.device != dev for t in xs):
         raise errors.InvalidArgumentError("batched encode: tensors must share dtype and device")
-    Ms = [torch.empty(t.shape, dtype=torch.int64, device=dev) for t in xs]
-    Es = [torch.empty(t.shape, dtype=torch.int64, device=dev) for t in xs]
+    Ms = _carve(xs, torch.int64, dev)
+    Es = _carve(xs, torch.int64, dev)
     tables = BatchTables(xs, Ms, Es)
     encode_batched_into(tables, code, decrease_precision, stream_handle(dev))
     return Ms, Es
 
 
-class BatchTables:
-    """Device pointer/length tables for the batched ABI (built once, reusable across launches)."""
+RUN_CHUNK = 1 << 20     # elements per entry of a coalesced table (BatchTables)
 
-    def __init__(self, srcs, d0s, d1s):
+
+def coalesce_runs(srcs, d0s, d1s, chunk=RUN_CHUNK):
+    """[(src_ptr, d0_ptr, d1_ptr, n)] of the batch with adjacent entries merged: entry i + 1 joins
+    entry i's run when each of its three buffers starts where entry i's ends (slices of one
+    embedding table, outputs carved from one buffer, or neighbours the caching allocator placed
+    back to back). The transform is element-wise, so a run is one tensor to the kernels. Runs
+    longer than `chunk` elements are cut into `chunk`-element pieces so the batched grid (count x
+    tiles of the longest entry) stays dense; empty entries are dropped."""
+    runs = []
+    for s, a, b in zip(srcs, d0s, d1s):
+        n = s.numel()
+        if n == 0:
+            continue
+        p = (s.data_ptr(), a.data_ptr(), b.data_ptr())
+        es = (s.element_size(), a.element_size(), b.element_size())
+        if runs:
+            r = runs[-1]
+            if all(p[i] == r[0][i] + r[1] * es[i] for i in range(3)):
+                r[1] += n
+                continue
+        runs.append([p, n, es])
+    out = []
+    for p, n, es in runs:
+        if n <= chunk:
+            out.append((p[0], p[1], p[2], n))
+            continue
+        for off in range(0, n, chunk):
+            out.append((p[0] + off * es[0], p[1] + off * es[1], p[2] + off * es[2], min(chunk, n - off)))
+    return out
+
+
+class BatchTables:
+    """Device pointer/length tables for the batched ABI (built once, reusable across launches).
+    coalesce=True merges adjacent entries into runs first (coalesce_runs); a batch that is one run
+    altogether goes through the streaming kernels (efl_fxp_encode / efl_fxp_decode) instead."""
+
+    def __init__(self, srcs, d0s, d1s, coalesce=True):
         dev = srcs[0].device
         self.keep = (srcs, d0s, d1s)
-        self.src = _ptr_table(srcs, dev)
-        self.d0 = _ptr_table(d0s, dev)
-        self.d1 = _ptr_table(d1s, dev)
-        self.ns = torch.tensor([t.numel() for t in srcs], dtype=torch.int64).to(dev)
-        self.count = len(srcs)
-        self.max_n = max(t.numel() for t in srcs)
+        if coalesce:
+            runs = coalesce_runs(srcs, d0s, d1s, chunk=1 << 62)
+            if len(runs) != 1:
+                runs = coalesce_runs(srcs, d0s, d1s)
+        else:
+            runs = [(s.data_ptr(), a.data_ptr(), b.data_ptr(), s.numel()) for s, a, b in zip(srcs, d0s, d1s)]
+        self.entries = len(srcs)
+        self.runs = runs
+        self.single = coalesce and len(runs) == 1
+        col = list(zip(*runs)) if runs else [[], [], [], []]
+        self.src, self.d0, self.d1, self.ns = (torch.tensor(list(c), dtype=torch.int64).to(dev) for c in col)
+        self.count = len(runs)
+        self.max_n = max((r[3] for r in runs), default=0)
 
     def args(self):
         return self.src.data_ptr(), self.d0.data_ptr(), self.d1.data_ptr(), self.ns.data_ptr(), \
@@ -315,16 +365,28 @@ class BatchTables:
 
 
 def encode_batched_into(tables: BatchTables, dtype_code: int, decrease_precision=False, stream=None):
+    stream = stream if stream is not None else stream_handle()
+    if tables.count == 0:
+        return
+    if tables.single:
+        s, a, b, n = tables.runs[0]
+        check(_lib.efl_fxp_encode(s, dtype_code, a, b, n, int(bool(decrease_precision)), stream))
+        return
     src, d0, d1, ns, count, max_n = tables.args()
     check(_lib.efl_fxp_encode_batched(src, dtype_code, d0, d1, ns, count, max_n,
-                                      int(bool(decrease_precision)),
-                                      stream if stream is not None else stream_handle()))
+                                      int(bool(decrease_precision)), stream))
 
 
 def decode_batched_into(tables: BatchTables, dtype_code: int, flags=0, stream=None):
+    stream = stream if stream is not None else stream_handle()
+    if tables.count == 0:
+        return
+    if tables.single:
+        m, e, y, n = tables.runs[0]
+        check(_lib.efl_fxp_decode(m, e, y, dtype_code, n, n, flags, stream))
+        return
     src, d0, d1, ns, count, max_n = tables.args()
-    check(_lib.efl_fxp_decode_batched(src, d0, d1, dtype_code, ns, count, max_n, flags,
-                                      stream if stream is not None else stream_handle()))
+    check(_lib.efl_fxp_decode_batched(src, d0, d1, dtype_code, ns, count, max_n, flags, stream))
 
 
 def fixed_point_to_float_point_batched(mantissas, exponents, dtype=torch.float32, flush_denormal=None):
@@ -352,7 +414,7 @@ def fixed_point_to_float_point_batched(mantissas, exponents, dtype=torch.float32
         ms.append(m.contiguous())
         es.append(e.contiguous())
     ftz = _flush_denormal if flush_denormal is None else bool(flush_denormal)
-    ys = [torch.empty(m.shape, dtype=dtype, device=dev) for m in ms]
+    ys = _carve(ms, dtype, dev)
     tables = BatchTables(ms, es, ys)
     decode_batched_into(tables, dt_code(dtype), 1 if ftz else 0, stream_handle(dev))
     return ys

@@ -67,6 +67,8 @@ for _name, _args in {
     "efl_pl_mul_scalar_big": [_vp, _PK, _vp, _vp, _i32, _vp, _vp, _i64, _vp, _vp],
     "efl_pl_fxp_add": [_vp, _PK, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp],
     "efl_pl_tune": [_i32, _i32, _i32],
+    "efl_host_powm": [_vp, _i32, _vp, _i32, _vp, _i32, _vp],
+    "efl_host_probable_primes": [_vp, _i32, _i32, _vp, _i32, _i32, _vp],
 }.items():
     getattr(_lib, _name).argtypes = _args
     getattr(_lib, _name).restype = _i32
@@ -186,52 +188,123 @@ def _int_of(v) -> int:
 _SMALL_PRIMES = [p for p in range(3, 2000) if all(p % d for d in range(2, int(p ** 0.5) + 1))]
 
 
+def _odd_primes_below(limit: int):
+    sieve = bytearray([1]) * limit
+    sieve[0:2] = b"\x00\x00"
+    for i in range(2, int(limit ** 0.5) + 1):
+        if sieve[i]:
+            sieve[i * i::i] = bytearray(len(range(i * i, limit, i)))
+    return [i for i in range(3, limit) if sieve[i]]
+
+
+# product of the odd primes below 2^16: one gcd per candidate (after the cheap trial division by
+# the primes below 2000) removes 40 % more composites than trial division alone before the
+# Miller-Rabin tests (the reference's mpz_probab_prime_p trial-divides first too)
+_SIEVE_PRODUCT = math.prod(p for p in _odd_primes_below(1 << 16) if p >= 2000)
+
+
+def _words(x: int, L: int) -> np.ndarray:
+    return np.frombuffer(x.to_bytes(4 * L, "little"), dtype="<u4")
+
+
+def host_powm(base: int, exp: int, mod: int) -> int:
+    """base^exp mod mod (odd mod, 0 <= base < mod) through efl_host_powm (native, host threads)."""
+    L = max(1, -(-mod.bit_length() // 32))
+    E = max(1, -(-exp.bit_length() // 32))
+    b, e, m = _words(base, L), _words(exp, E), _words(mod, L)
+    out = np.empty(L, dtype="<u4")
+    _efl_lib.check(_lib.efl_host_powm(b.ctypes.data, L, e.ctypes.data, E, m.ctypes.data, L, out.ctypes.data))
+    return int.from_bytes(out.tobytes(), "little")
+
+
+def _sieved(c: int) -> bool:
+    for p in _SMALL_PRIMES:
+        if c % p == 0:
+            return False
+    return math.gcd(_SIEVE_PRODUCT % c, c) == 1
+
+
+def _mr(cands, bases_per, threads=0):
+    """efl_host_probable_primes over (candidate, [bases]) pairs; list of bools."""
+    L = max(-(-c.bit_length() // 32) for c in cands)
+    reps = len(bases_per[0])
+    C = np.stack([_words(c, L) for c in cands])
+    B = np.stack([np.stack([_words(b, L) for b in bs]) for bs in bases_per])
+    out = np.zeros(len(cands), dtype=np.int8)
+    _efl_lib.check(_lib.efl_host_probable_primes(C.ctypes.data, L, len(cands), B.ctypes.data, reps, threads,
+                                                 out.ctypes.data))
+    return [bool(v) for v in out]
+
+
+def probable_primes(cands, reps: int, rng, threads: int = 0):
+    """Miller-Rabin with `reps` random bases each (drawn from rng in candidate order, then round
+    order) for odd candidates > 3, on host threads in native code (efl_host_probable_primes): one
+    round for every candidate first (almost every composite fails it), then the remaining rounds of
+    the survivors side by side, one (candidate, base) per work item. Returns a list of bools."""
+    if not cands:
+        return []
+    bases = [[rng.randrange(2, c - 1) for _ in range(reps)] for c in cands]
+    ok = _mr(cands, [b[:1] for b in bases], threads)
+    rest = [(i, b) for i, c in enumerate(cands) if ok[i] for b in bases[i][1:]]
+    if rest:
+        res = _mr([cands[i] for i, _ in rest], [[b] for _, b in rest], threads)
+        for (i, _), r in zip(rest, res):
+            ok[i] = ok[i] and r
+    return ok
+
+
 def _probable_prime(x: int, reps: int, rng) -> bool:
     if x < 2:
         return False
     for p in _SMALL_PRIMES:
         if x % p == 0:
             return x == p
-    d, s = x - 1, 0
-    while d % 2 == 0:
-        d //= 2
-        s += 1
-    for _ in range(reps):
-        a = rng.randrange(2, x - 1)
-        y = pow(a, d, x)
-        if y in (1, x - 1):
-            continue
-        for _ in range(s - 1):
-            y = y * y % x
-            if y == x - 1:
-                break
-        else:
-            return False
-    return True
+    return probable_primes([x], reps, rng)[0]
 
 
-def generate_keypair_ints(n_bytes=512, reps=24, rng=None):
-    """(n, hs, p, q) with the reference's construction: primes of n_bytes*4 bits with bits 0, 1
-    and the top bit set, gcd(p-1, q-1) = 2, hs = (-x^2)^n mod n^2 for a random x in Z_n^*."""
+def generate_keypair_ints(n_bytes=512, reps=24, rng=None, batch=None):
+    """(n, hs, p, q) with the reference's construction (GeneratePaillierKeypairOp,
+    paillier.cc:851-888): primes of n_bytes*4 bits drawn uniformly with bits 0, 1 and the top bit
+    set, gcd(p-1, q-1) = 2, hs = (-x^2)^n mod n^2 for a random x in Z_n^*.
+
+    Candidates are drawn `batch` at a time; trial division and one gcd against the product of the
+    odd primes below 2^16 discard most composites on the host, a q candidate with
+    gcd(p-1, q-1) != 2 is discarded before any primality test (the reference draws both primes
+    again instead: the same distribution of accepted pairs, given p), and the survivors of a batch
+    get their `reps` Miller-Rabin rounds on host threads in native code (efl_host_probable_primes);
+    the first probable prime in draw order is taken. hs is computed by CRT mod p^2 and q^2
+    (efl_host_powm) and joined: the same value as the reference's mpz_powm mod n^2."""
     rng = rng or secrets.SystemRandom()
     bits = n_bytes * 4
+    if batch is None:
+        batch = 64 if bits >= 1024 else 16
 
-    def draw():
+    def draw(accept=None):
         while True:
-            c = rng.getrandbits(bits) | 3 | (1 << (bits - 1))
-            if _probable_prime(c, reps, rng):
-                return c
-    while True:
-        p, q = draw(), draw()
-        if math.gcd(p - 1, q - 1) == 2 and p != q:
-            break
+            cs = [rng.getrandbits(bits) | 3 | (1 << (bits - 1)) for _ in range(batch)]
+            cs = [c for c in cs if _sieved(c) and (accept is None or accept(c))]
+            for c, ok in zip(cs, probable_primes(cs, reps, rng)):
+                if ok:
+                    return c
+    p = draw()
+    q = draw(lambda c: c != p and math.gcd(p - 1, c - 1) == 2)
     n = p * q
     while True:
         x = rng.randrange(1, n)
         if math.gcd(x, n) == 1:
             break
-    hs = pow((-x * x) % n, n, n * n)
-    return n, hs, p, q
+    return n, hs_of(x, p, q), p, q
+
+
+def hs_of(x: int, p: int, q: int) -> int:
+    """(-x^2)^n mod n^2 (paillier.cc:884-888) by CRT: the powers mod p^2 and mod q^2 (exponent n
+    reduced mod p (p - 1), the order of Z_(p^2)^*) through efl_host_powm, joined by Garner."""
+    n = p * q
+    h = (-x * x) % n
+    p2, q2 = p * p, q * q
+    hp = host_powm(h % p2, n % (p * (p - 1)), p2)
+    hq = host_powm(h % q2, n % (q * (q - 1)), q2)
+    return (hp + p2 * ((hq - hp) * pow(p2, -1, q2) % q2)) % (n * n)
 
 
 # ----------------------------------------------------------------------------------------------

@@ -322,6 +322,19 @@ int efl_hex_parse(const char* chars, const int64_t* offsets, int limbs_per_elem,
 int efl_pl_to_int64(const uint32_t* magnitude, int limbs_per_elem, const int8_t* negative,
                     int64_t* out, int64_t n, void* stream);
 
+/* ---- Key generation, HOST memory (GeneratePaillierKeypairOp, paillier.cc:833-904) ------------
+ * The reference's keygen is a CPU op over GMP (mpz_probab_prime_p in find_prime, :851-863;
+ * mpz_powm for hs, :884-888). These two are its arithmetic, on host buffers of little-endian
+ * 32-bit words; the caller draws and sieves the candidates (efl/privacy/paillier_cipher.py). */
+/* out = base^exp mod mod, mod odd, base < mod; out has mod_words words. */
+int efl_host_powm(const uint32_t* base, int base_words, const uint32_t* exp, int exp_words,
+                  const uint32_t* mod, int mod_words, uint32_t* out);
+/* Miller-Rabin of `count` odd candidates > 3 ([count][words]) with `reps` bases each
+ * ([count][reps][words], in [2, c - 2]): out[i] = 1 probable prime, 0 composite; `threads` host
+ * threads (<= 0: all). */
+int efl_host_probable_primes(const uint32_t* cands, int words, int count, const uint32_t* bases, int reps,
+                             int threads, int8_t* out);
+
 /* ---- Secret-sharing masks -------------------------------------------------
  * Replace the per-element float work of efls-train/python/efl/privacy/secret_sharing.py, whose
  * noise is generate_suitable_noise(t) = tf.random.uniform(shape(t)) * t (:26-27). The uniform is
