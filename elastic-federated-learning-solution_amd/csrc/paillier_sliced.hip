@@ -152,6 +152,9 @@ __device__ __forceinline__ void fbpowm_mont(uint32_t (&acc)[C], const Key& k, ui
 #ifndef EFL_MAT_WAVES32
 #define EFL_MAT_WAVES32 2
 #endif
+#ifndef EFL_WALK_PROBE
+#define EFL_WALK_PROBE 0
+#endif
 #ifndef EFL_MAT_PREFETCH
 #define EFL_MAT_PREFETCH 0
 #endif
@@ -237,7 +240,11 @@ __device__ __forceinline__ void fbpowm28_walk(uint32_t (&acc)[s28::limbs_per_lan
   for (int s = 0, row = 0; s < size; s += W, ++row) {
     const uint32_t idx = col_bits(A, E, s, size - s < W ? size - s : W, words);
     if (idx) {
+#if EFL_WALK_PROBE   // latency probe build (tools/walk_probe.py): every product reads entry (0, 0), L2-resident
+      const uint32_t* ent = table + g * C28;
+#else
       const uint32_t* ent = table + ((int64_t)row * cols + (idx - 1)) * L28 + g * C28;
+#endif
 #pragma unroll
       for (int j = 0; j < C28; ++j) B[(g * C28 + j) * E] = ent[j];
       lds_sync();

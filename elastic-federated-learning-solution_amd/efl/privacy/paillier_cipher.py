@@ -328,6 +328,7 @@ class KeyBlock:
             p, q = q, p        # CRT below reduces mq mod p with one subtraction: needs q < 2p
         self.n, self.hs, self.p, self.q = n, hs, p, q
         self.a_bits, self.group_size = a_bits, group_size
+        self._window_arg = table_window     # an explicit window also sizes the CRT sub-tables
         need = max(n.bit_length(), 2 * max(p or 0, q or 0).bit_length())
         ln = next((c for c in _LIMB_CLASSES if 32 * c >= need), None)
         if ln is None:
@@ -497,7 +498,7 @@ class KeyBlock:
                     # v = q^2 yp + p^2 yq mod n^2 = hs^(a') R then needs no modular product, and
                     # g(m) hs^(a') = mont(g(m), v) is one
                     subs.append(KeyBlock(x, self.hs % (x * x), self.a_bits, self.group_size, device=self.device,
-                                         walk_start=start))
+                                         walk_start=start, table_window=self._window_arg))
                 self._crt = tuple(subs)
         return self._crt or None
 

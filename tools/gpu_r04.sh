@@ -1,0 +1,45 @@
+#!/bin/bash
+# Round-4 GPU session script: each GPU step under its own time limit, chained, output under
+# gpurun_out/. Usage: bash tools/gpu_r04.sh <step>...
+set -o pipefail
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+export PYTHONUNBUFFERED=1
+LIBDIR=$PWD/elastic-federated-learning-solution_amd/efl
+run() {
+  case "$1" in
+    tests)  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+              > gpurun_out/r04_pytest.log 2>&1 ;;
+    smoke)  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r04_smoke.log 2>&1 ;;
+    bench)  timeout -k 10 400 python -u bench.py > gpurun_out/r04_bench.json 2> gpurun_out/r04_bench.err ;;
+    bench2) timeout -k 10 300 python -u bench.py --gpus 2 --steps 20 --warmup 3 --no-extras --no-cpu-baseline \
+              > gpurun_out/r04_bench_gpus2.json 2> gpurun_out/r04_bench_gpus2.err ;;
+    prof)   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r04_prof_trace -o run --output-format csv \
+              -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-extras > gpurun_out/r04_prof_trace.log 2>&1 ;;
+    pmc)    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/r04_prof_fetch -o run --output-format csv \
+              -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-extras > gpurun_out/r04_prof_fetch.log 2>&1 && \
+            timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/r04_prof_write -o run --output-format csv \
+              -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-extras > gpurun_out/r04_prof_write.log 2>&1 ;;
+    stagep) timeout -k 10 1000 python -u bench.py --stage p > gpurun_out/r04_stage_p.jsonl 2> gpurun_out/r04_stage_p.err ;;
+    stagepq) timeout -k 10 600 python -u bench.py --stage p --no-cpu-baseline > gpurun_out/r04_stage_p.jsonl 2> gpurun_out/r04_stage_p.err ;;
+    layer)  timeout -k 10 400 python -u tools/bench_layer.py --steps 3 --warmup 1 > gpurun_out/r04_layer_dense.jsonl 2> gpurun_out/r04_layer_dense.err && \
+            timeout -k 10 400 python -u tools/bench_layer.py --steps 3 --warmup 1 --kind weight > gpurun_out/r04_layer_weight.jsonl 2> gpurun_out/r04_layer_weight.err ;;
+    c3co)   timeout -k 10 300 python -u tools/config3_coalesce_probe.py > gpurun_out/r04_c3_coalesce.jsonl 2> gpurun_out/r04_c3_coalesce.err ;;
+    c3kt)   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/r04_c3_kt -o run --output-format csv \
+              -- python3 tools/config3_probe.py --reps 20 > gpurun_out/r04_c3_kt.log 2>&1 && \
+            cp /tmp/r04_c3_kt/run_kernel_stats.csv gpurun_out/r04_c3_kernel_stats.csv ;;
+    walk)   for lib in ${WALK_LIBS:-libefl_hip.so}; do
+              EFL_HIP_LIB=$LIBDIR/$lib timeout -k 10 200 python -u tools/walk_probe.py >> gpurun_out/r04_walk_probe.jsonl \
+                2>> gpurun_out/r04_walk_probe.err || return $?
+            done ;;
+    rekey)  timeout -k 10 300 python -u tools/rekey_probe.py > gpurun_out/r04_rekey.jsonl 2> gpurun_out/r04_rekey.err ;;
+    decfam) timeout -k 10 600 python -u tools/sweep_dec_family.py > gpurun_out/r04_dec_family.jsonl 2> gpurun_out/r04_dec_family.err ;;
+    *) echo "unknown step $1"; return 2 ;;
+  esac
+}
+for s in "$@"; do
+  echo "== $s $(date +%T)"
+  run "$s" || { rc=$?; echo "step $s failed rc=$rc"; exit $rc; }
+done
+echo "== done $(date +%T)"

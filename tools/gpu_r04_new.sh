@@ -14,4 +14,9 @@ tail -30 gpurun_out/r04_new.log
 timeout -k 10 300 python -u tools/config3_coalesce_probe.py > gpurun_out/c3_coalesce.jsonl 2> gpurun_out/c3_coalesce.err
 rc=$?
 cat gpurun_out/c3_coalesce.jsonl; tail -5 gpurun_out/c3_coalesce.err
-exit $rc
+[ $rc -eq 0 ] || exit $rc
+for lib in libefl_hip.so libefl_hip_wprobe.so libefl_hip.so; do
+  EFL_HIP_LIB=$PWD/elastic-federated-learning-solution_amd/efl/$lib timeout -k 10 200 python -u tools/walk_probe.py \
+    >> gpurun_out/walk_probe.jsonl 2>> gpurun_out/walk_probe.err || exit $?
+done
+cat gpurun_out/walk_probe.jsonl
