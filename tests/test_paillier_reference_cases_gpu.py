@@ -25,7 +25,9 @@ def kp():
     efl.lib.require_gpu()
     k = efl.paillier.Keypair()
     k.generate_keypair()                     # reference defaults: 4096-bit n, 2048-bit a, g = 1
-    assert k.key.n.bit_length() == 4096 and k.key.a_bits == 2048 and k.key.group_size == 1
+    # two 2048-bit primes: n has 4095 or 4096 bits (paillier.cc:851-877), the 4096-bit limb class
+    assert k.key.n.bit_length() in (4095, 4096) and k.key.ln == 128
+    assert k.key.a_bits == 2048 and k.key.group_size == 1
     return k
 
 
