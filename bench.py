@@ -142,17 +142,27 @@ def cpu_baseline(x_dev, threads, how, ftz):
             "ms_per_step": round(t * 1e3, 2)}
 
 
-def config3(efl, dev, steps):
-    """BASELINE config 3: 4096 separate 64 KiB fp32 tensors ([128, 128] embedding slices,
-    N(0, 0.01), seed 1): one batched encode + one batched decode launch over device pointer
-    tables, against the naive 2 x 4096 per-slice launches."""
+def config3(efl, dev, steps, layout="separate"):
+    """BASELINE config 3: 4096 64 KiB fp32 tensors ([128, 128] embedding slices, N(0, 0.01),
+    seed 1): one batched encode + one batched decode launch over device pointer tables, against
+    the naive 2 x 4096 per-slice launches. layout "separate": 4 x 4096 torch allocations (each
+    slice its own tensor); "views": the slices are views of one [4096, 128, 128] table per stream
+    (embedding slices of one table), which efl.lib.BatchTables sends through the streaming kernels
+    as one run."""
     lib = efl.lib.raw()
     slices, elems = 4096, 16384
     g = torch.Generator(device=dev).manual_seed(1)
-    xs = [torch.randn(128, 128, device=dev, generator=g) * 0.01 for _ in range(slices)]
-    Ms = [torch.empty(128, 128, dtype=torch.int64, device=dev) for _ in range(slices)]
-    Es = [torch.empty(128, 128, dtype=torch.int64, device=dev) for _ in range(slices)]
-    ys = [torch.empty(128, 128, device=dev) for _ in range(slices)]
+    if layout == "views":
+        big = (torch.randn(slices, 128, 128, device=dev, generator=g) * 0.01,
+               torch.empty(slices, 128, 128, dtype=torch.int64, device=dev),
+               torch.empty(slices, 128, 128, dtype=torch.int64, device=dev),
+               torch.empty(slices, 128, 128, device=dev))
+        xs, Ms, Es, ys = ([b[i] for i in range(slices)] for b in big)
+    else:
+        xs = [torch.randn(128, 128, device=dev, generator=g) * 0.01 for _ in range(slices)]
+        Ms = [torch.empty(128, 128, dtype=torch.int64, device=dev) for _ in range(slices)]
+        Es = [torch.empty(128, 128, dtype=torch.int64, device=dev) for _ in range(slices)]
+        ys = [torch.empty(128, 128, device=dev) for _ in range(slices)]
     enc_t = efl.lib.BatchTables(xs, Ms, Es)
     dec_t = efl.lib.BatchTables(Ms, Es, ys)
     stream = torch.cuda.current_stream(dev)
@@ -181,13 +191,17 @@ def config3(efl, dev, steps):
 
     t_b = wall(batched, max(10, steps))
     ok = all(torch.equal(x, y) for x, y in zip(xs[::64], ys[::64]))
-    t_n = wall(naive, 3)
     nbytes = slices * elems * 4
-    return {"workload": "config 3: 4096 x 64 KiB fp32 slices [128,128], batched encode+decode",
-            "GiBs": round(nbytes / GIB / t_b, 2), "ms": round(t_b * 1e3, 4),
-            "hbm_frac": round(2 * BYTES_PER_ELEM_KERNEL * slices * elems / t_b / 1e9 / PEAK_HBM_GBS, 4),
-            "naive_per_slice_ms": round(t_n * 1e3, 3), "naive_GiBs": round(nbytes / GIB / t_n, 3),
-            "launches": {"batched": 2, "naive": 2 * slices}, "roundtrip_ok": ok}
+    out = {"workload": f"config 3: 4096 x 64 KiB fp32 slices [128,128] ({layout}), batched encode+decode",
+           "GiBs": round(nbytes / GIB / t_b, 2), "ms": round(t_b * 1e3, 4),
+           "hbm_frac": round(2 * BYTES_PER_ELEM_KERNEL * slices * elems / t_b / 1e9 / PEAK_HBM_GBS, 4),
+           "table_entries": {"encode": enc_t.count, "decode": dec_t.count},
+           "launches": {"batched": 2}, "roundtrip_ok": ok}
+    if layout == "separate":
+        t_n = wall(naive, 3)
+        out.update({"naive_per_slice_ms": round(t_n * 1e3, 3), "naive_GiBs": round(nbytes / GIB / t_n, 3)})
+        out["launches"]["naive"] = 2 * slices
+    return out
 
 
 def pinned_path(efl, dev, x_dev, reps=3):
@@ -808,6 +822,7 @@ def main(argv=None):
     if world == 1 and not args.no_extras:
         del M, E, y
         out["config3"] = config3(efl, dev, args.steps)
+        out["config3"]["views"] = config3(efl, dev, args.steps, layout="views")
         out["pinned_path"] = pinned_path(efl, dev, x)
         out["config5"] = config5()
     if world == 1 and not args.no_cpu_baseline:

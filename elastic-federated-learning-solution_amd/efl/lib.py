@@ -339,21 +339,30 @@ def coalesce_runs(srcs, d0s, d1s, chunk=RUN_CHUNK):
 
 class BatchTables:
     """Device pointer/length tables for the batched ABI (built once, reusable across launches).
-    coalesce=True merges adjacent entries into runs first (coalesce_runs); a batch that is one run
-    altogether goes through the streaming kernels (efl_fxp_encode / efl_fxp_decode) instead."""
 
-    def __init__(self, srcs, d0s, d1s, coalesce=True):
+    coalesce: "single" (default) sends a batch whose slices form ONE run in all three streams
+    (slices of one embedding table with outputs carved from one buffer, coalesce_runs) through the
+    streaming kernels (efl_fxp_encode / efl_fxp_decode) and keeps one table entry per slice
+    otherwise; True merges every run (cut into RUN_CHUNK pieces); False keeps one entry per slice.
+    Measured on MI355X (tools/config3_coalesce_probe.py, profiles/r04/c3_coalesce.jsonl), config 3's
+    4096 x 64 KiB slices: views of one table 0.753 of HBM per slice -> 0.837 as one run; the bench's
+    4096 separate allocations (384 runs of ~11 slices) 0.820 per slice against 0.811 merged."""
+
+    def __init__(self, srcs, d0s, d1s, coalesce="single"):
         dev = srcs[0].device
         self.keep = (srcs, d0s, d1s)
+        runs = None
         if coalesce:
-            runs = coalesce_runs(srcs, d0s, d1s, chunk=1 << 62)
-            if len(runs) != 1:
+            merged = coalesce_runs(srcs, d0s, d1s, chunk=1 << 62)
+            if len(merged) == 1:
+                runs = merged
+            elif coalesce is True:
                 runs = coalesce_runs(srcs, d0s, d1s)
-        else:
+        if runs is None:
             runs = [(s.data_ptr(), a.data_ptr(), b.data_ptr(), s.numel()) for s, a, b in zip(srcs, d0s, d1s)]
         self.entries = len(srcs)
         self.runs = runs
-        self.single = coalesce and len(runs) == 1
+        self.single = bool(coalesce) and len(runs) == 1
         col = list(zip(*runs)) if runs else [[], [], [], []]
         self.src, self.d0, self.d1, self.ns = (torch.tensor(list(c), dtype=torch.int64).to(dev) for c in col)
         self.count = len(runs)
