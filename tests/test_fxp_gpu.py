@@ -358,9 +358,9 @@ def test_batched_embedding_slices(efl):
 @pytest.mark.parametrize("coalesce", ["single", True, False])
 def test_batched_tables_coalescing_identical(efl, coalesce):
     """BatchTables over slices of one table: as one run through the streaming kernels ("single",
-    the default when the slices are adjacent in all three streams), as merged chunked runs (True),
-    and one entry per slice through the batched kernels (False): the same bits. With a gap in the
-    output buffer the batch is no longer one run and takes the batched kernels."""
+    the default, and True when the slices are adjacent in all three streams) and one entry per slice
+    through the batched kernels (False): the same bits. With a gap in one output buffer the batch
+    is two runs: merged into two entries (True) or one entry per slice, batched kernels both."""
     S, n = 300, 5000
     g = torch.Generator(device="cuda").manual_seed(7)
     x = torch.randn(S * n, device="cuda", generator=g)
@@ -371,17 +371,18 @@ def test_batched_tables_coalescing_identical(efl, coalesce):
     xs, Ms, Es, ys = ([b[i * n:(i + 1) * n] for i in range(S)] for b in (x, M, E, y))
     enc = efl.lib.BatchTables(xs, Ms, Es, coalesce=coalesce)
     dec = efl.lib.BatchTables(Ms, Es, ys, coalesce=coalesce)
-    assert enc.single == (coalesce == "single") and enc.count == {"single": 1, True: 2, False: S}[coalesce]
+    assert enc.single == (coalesce in ("single", True)) and enc.count == {"single": 1, True: 1, False: S}[coalesce]
     efl.lib.encode_batched_into(enc, 1)
     efl.lib.decode_batched_into(dec, 1, 1)
     Mo, Eo = fxp.encode(host(x))
     assert np.array_equal(host(M), Mo) and np.array_equal(host(E), Eo)
     assert np.array_equal(bits32(y), fxp.decode(Mo, Eo).view(np.uint32))
-    # a gap in one output stream: not a run
+    # a gap in one output stream: two runs (merged and chunked with coalesce=True, else one entry
+    # per slice), through the batched kernels
     M2 = torch.empty(S * n + 2, dtype=torch.int64, device="cuda")
     gap = [M2[i * n + (2 if i >= S // 2 else 0):][:n] for i in range(S)]
-    t = efl.lib.BatchTables(xs, gap, Es)
-    assert not t.single and t.count == S
+    t = efl.lib.BatchTables(xs, gap, Es, coalesce=coalesce)
+    assert not t.single and t.count == (2 if coalesce is True else S)
     efl.lib.encode_batched_into(t, 1)
     assert np.array_equal(np.concatenate([host(m) for m in gap]), Mo)
 
