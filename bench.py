@@ -402,6 +402,9 @@ def stage_p(args):
             out["cpu_baseline"] = stage_p_cpu(n_bytes, a_bytes, g, p, q, hs, args.cpu_threads, cpu_keys)
             for name in ("encrypt", "decrypt"):
                 out[name]["vs_cpu"] = round(out[name]["elements_per_s"] / out["cpu_baseline"][name], 1)
+            if "encrypt_crt" in out:      # the same op (PaillierEncrypt) for the key owner
+                out["encrypt_crt"]["vs_cpu"] = round(out["encrypt_crt"]["elements_per_s"] /
+                                                     out["cpu_baseline"]["encrypt"], 1)
         if "MNIST" in label:
             out["matmul"] = stage_p_matmul(args, efl, pc, kp, lib, sh, stream, dev)
         print(json.dumps(out), flush=True)
