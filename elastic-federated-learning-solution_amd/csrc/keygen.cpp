@@ -197,6 +197,39 @@ EFL_API int efl_host_powm(const uint32_t* base, int base_words, const uint32_t* 
   return 0;
 }
 
+// The fixed-base table's row bases (gmp_utils.cc:73-88 raises the base by 2^W per row):
+// out[i] = base^(2^(k i)) mod mod for i in [0, steps), mod odd, base < mod; out is [steps][mod_words].
+// One Montgomery setup for the whole chain of k (steps - 1) squarings.
+EFL_API int efl_host_sqr_chain(const uint32_t* base, int base_words, int k, int steps, const uint32_t* mod,
+                               int mod_words, uint32_t* out) {
+  if (!base || !mod || !out || mod_words <= 0 || base_words < 0 || base_words > mod_words || k < 0 || steps < 0) {
+    efl::set_error("efl_host_sqr_chain: bad arguments");
+    return EFL_E_INVALID_ARGUMENT;
+  }
+  if (!(mod[0] & 1)) {
+    efl::set_error("efl_host_sqr_chain: the modulus must be odd");
+    return EFL_E_INVALID_ARGUMENT;
+  }
+  const int L = (mod_words + 1) / 2;
+  const std::vector<uint64_t> m = to64(mod, mod_words, L), b = to64(base, base_words, L);
+  if (Mont::geq(b.data(), m.data(), L)) {
+    efl::set_error("efl_host_sqr_chain: base must be below the modulus");
+    return EFL_E_INVALID_ARGUMENT;
+  }
+  Mont M(m);
+  std::vector<uint64_t> x(L), y(L), one(L, 0);
+  one[0] = 1;
+  M.mul(x.data(), b.data(), M.r2.data());      // base R
+  for (int i = 0; i < steps; ++i) {
+    if (i)
+      for (int s = 0; s < k; ++s) M.mul(x.data(), x.data(), x.data());
+    M.mul(y.data(), x.data(), one.data());      // out of Montgomery form
+    uint32_t* o = out + (size_t)i * mod_words;
+    for (int j = 0; j < mod_words; ++j) o[j] = (uint32_t)(y[j >> 1] >> (32 * (j & 1)));
+  }
+  return 0;
+}
+
 // Miller-Rabin of `count` odd candidates ([count][words] 32-bit words, each > 3) with `reps` bases
 // each ([count][reps][words], in [2, c - 2]); out[i] = 1 probable prime, 0 composite. Candidates
 // are shared out over `threads` host threads (<= 0: hardware concurrency).

@@ -68,6 +68,7 @@ for _name, _args in {
     "efl_pl_fxp_add": [_vp, _PK, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp],
     "efl_pl_tune": [_i32, _i32, _i32],
     "efl_host_powm": [_vp, _i32, _vp, _i32, _vp, _i32, _vp],
+    "efl_host_sqr_chain": [_vp, _i32, _i32, _i32, _vp, _i32, _vp],
     "efl_host_probable_primes": [_vp, _i32, _i32, _vp, _i32, _i32, _vp],
 }.items():
     getattr(_lib, _name).argtypes = _args
@@ -215,6 +216,15 @@ def host_powm(base: int, exp: int, mod: int) -> int:
     out = np.empty(L, dtype="<u4")
     _efl_lib.check(_lib.efl_host_powm(b.ctypes.data, L, e.ctypes.data, E, m.ctypes.data, L, out.ctypes.data))
     return int.from_bytes(out.tobytes(), "little")
+
+
+def host_sqr_chain(base: int, k: int, steps: int, mod: int, words: int) -> np.ndarray:
+    """[steps, words] little-endian uint32 rows base^(2^(k i)) mod mod (odd mod, base < mod):
+    the fixed-base table's row bases, one native call (efl_host_sqr_chain)."""
+    b, m = _words(base, words), _words(mod, words)
+    out = np.empty((steps, words), dtype="<u4")
+    _efl_lib.check(_lib.efl_host_sqr_chain(b.ctypes.data, words, k, steps, m.ctypes.data, words, out.ctypes.data))
+    return out
 
 
 def _sieved(c: int) -> bool:
@@ -508,16 +518,13 @@ class KeyBlock:
         [rows, cols, L28] limbs). Row bases hs^(2^(W i)) come from W squarings each on the host;
         every entry is then one short GPU exponentiation base_i^j (efl_pl_powm, W-bit exponents)
         and one GPU product by R (or R28) mod n^2 (efl_pl_add) — the work the reference does with
-        mpz_mul per entry when a keypair is set (gmp_utils.cc:73-88)."""
+        mpz_mul per entry when a keypair is set (gmp_utils.cc:73-88). The row bases come from one
+        native host call (efl_host_sqr_chain: 0.38 s of CPython pow for the 4096-bit key's 170 x 12
+        squarings mod n^2)."""
         dev, lc = self.device, self.lc
         sh = _stream(dev)
-        bases = []
-        b = hs
-        for i in range(rows):
-            bases.append(b)
-            if i + 1 < rows:
-                b = pow(b, 1 << W, n2)
-        bases_d = torch.from_numpy(np.stack([_limbs(v, lc) for v in bases]).view(np.int32)).to(dev)
+        # hs^(2^(W i)) for every row: W squarings per row, on the host in native code
+        bases_d = torch.from_numpy(host_sqr_chain(hs, W, rows, n2, lc).view(np.int32)).to(dev)
         t32 = torch.empty((rows, cols, lc), dtype=torch.int32, device=dev)
         t28 = torch.empty((rows, cols, L28), dtype=torch.int32, device=dev) if L28 else None
         exps = torch.arange(1, cols + 1, dtype=torch.int32, device=dev)
@@ -723,8 +730,16 @@ class PaillierKeypair(object):
         self._set(n, n_bytes or (n.bit_length() + 7) // 8, hs, a_bytes, group_size, p, q, table_window)
 
     def _set(self, n, n_bytes, hs, a_bytes, group_size, p=None, q=None, table_window=None):
+        old = self._key
+        if old is not None and (old.n, old.hs) != (n, hs):
+            # a new public key (a re-key): nothing of the old block can be reused, so the keypair
+            # lets go of it, and of the key owner's CRT sub-tables, before the new table is built.
+            # Ciphertexts that still reference the old block keep it alive; its sub-tables only
+            # ever served this keypair's own encryptions.
+            old._crt = None
+            self._key = old = None
         self._key = KeyBlock(n, hs, 8 * int(a_bytes), int(group_size), p, q, table_window=table_window,
-                             reuse_table=self._key)
+                             reuse_table=old)
         self._n_bytes = n_bytes
 
     @property

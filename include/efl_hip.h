@@ -329,6 +329,11 @@ int efl_pl_to_int64(const uint32_t* magnitude, int limbs_per_elem, const int8_t*
 /* out = base^exp mod mod, mod odd, base < mod; out has mod_words words. */
 int efl_host_powm(const uint32_t* base, int base_words, const uint32_t* exp, int exp_words,
                   const uint32_t* mod, int mod_words, uint32_t* out);
+/* Row bases of the fixed-base table (gmp_utils.cc:73-88): out[i] = base^(2^(k i)) mod mod for
+ * i < steps ([steps][mod_words] words), mod odd, base < mod; KeyBlock builds every entry from them
+ * on the device. */
+int efl_host_sqr_chain(const uint32_t* base, int base_words, int k, int steps, const uint32_t* mod,
+                       int mod_words, uint32_t* out);
 /* Miller-Rabin of `count` odd candidates > 3 ([count][words]) with `reps` bases each
  * ([count][reps][words], in [2, c - 2]): out[i] = 1 probable prime, 0 composite; `threads` host
  * threads (<= 0: all). */

@@ -79,3 +79,21 @@ def test_hs_by_crt_equals_direct_power():
     for _ in range(5):
         x = r.randrange(1, n)
         assert pc.hs_of(x, p, q) == pow((-x * x) % n, n, n * n)
+
+
+def test_host_sqr_chain_matches_repeated_powers():
+    """The fixed-base table's row bases (efl_host_sqr_chain): base^(2^(k i)) mod m, as KeyBlock's
+    table build takes them, for odd moduli of 1 to 128 words and k = 0, 1, 12."""
+    r = random.Random(3)
+    for words in (1, 2, 33, 128):
+        m = r.getrandbits(32 * words) | 1 | (1 << (32 * words - 1))
+        b = r.randrange(m)
+        for k in (0, 1, 12):
+            rows = pc.host_sqr_chain(b, k, 7, m, words)
+            x = b
+            for row in rows:
+                assert int.from_bytes(row.tobytes(), "little") == x
+                x = pow(x, 1 << k, m)
+    from efl import errors
+    with pytest.raises(errors.InvalidArgumentError):
+        pc.host_sqr_chain(5, 1, 2, 10, 1)
