@@ -106,7 +106,9 @@ SLICINGS = {16: ([0, 8, 16, 32], [0, 8]), 32: ([0, 8, 16, 32], [0, 8, 16, 32]), 
 
 _LIMB_CLASSES = (16, 32, 64, 128)
 MAX_TABLE_BITS = 1 << 40      # gmp_utils.h:20 FBPOWM_MAX_TABLE_MEM, compared against entries x bits
-TABLE28_MAX_BYTES = 1 << 30   # above this the radix-2^28 copy of the fixed-base table is not built
+# above this the radix-2^28 copy of the fixed-base table is not built (a table chosen under
+# TABLE_MAX_BYTES always has it; an explicit table_window up to 24 may ask for more)
+TABLE28_MAX_BYTES = 1 << 36
 
 
 def _limbs28_rows(vals, L: int, nbytes: int) -> np.ndarray:
@@ -418,8 +420,8 @@ class KeyBlock:
         fam = kernel_slicing(ln, False)
         L28 = limbs28_total(2 * ln, 2 * ln // fam) if fam else 0
         W = int(table_window) if table_window else choose_table_window(a_bits, 4 * (self.lc + L28))
-        if not 1 <= W <= 16:
-            raise errors.InvalidArgumentError("table_window must be in [1, 16]")
+        if not 1 <= W <= 24:
+            raise errors.InvalidArgumentError("table_window must be in [1, 24]")
         cols = (1 << W) - 1
         rows = -(-a_bits // W)
         d.table_rows, d.table_cols, d.table_window = rows, cols, W

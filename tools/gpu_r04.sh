@@ -37,6 +37,10 @@ run() {
                 2>> gpurun_out/r04_walk_probe.err || return $?
             done ;;
     rekey)  timeout -k 10 300 python -u tools/rekey_probe.py > gpurun_out/r04_rekey.jsonl 2> gpurun_out/r04_rekey.err ;;
+    tblw)   timeout -k 10 600 python -u tools/table_window_probe.py --crt 16 18 20 \
+              > gpurun_out/r04_table_window_1024.jsonl 2> gpurun_out/r04_table_window_1024.err && \
+            timeout -k 10 600 python -u tools/table_window_probe.py --crt --n-bytes 512 --a-bytes 256 --group 1 --sizes 65536 12 14 15 \
+              > gpurun_out/r04_table_window_4096.jsonl 2> gpurun_out/r04_table_window_4096.err ;;
     decfam) timeout -k 10 600 python -u tools/sweep_dec_family.py > gpurun_out/r04_dec_family.jsonl 2> gpurun_out/r04_dec_family.err ;;
     *) echo "unknown step $1"; return 2 ;;
   esac

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--a-bytes", type=int, default=64)
     ap.add_argument("--group", type=int, default=10)
     ap.add_argument("--sizes", type=int, nargs="+", default=[262144, 100352])
+    ap.add_argument("--crt", action="store_true", help="also time the key owner's encryption by CRT")
     ap.add_argument("windows", type=int, nargs="*", default=[12, 13, 14, 15, 16])
     a = ap.parse_args()
     n_bytes, a_bytes, g = a.n_bytes, a.a_bytes, a.group
@@ -64,8 +65,30 @@ def main():
             c = min(N, 256)
             got = kp.decrypt(pc.CipherTensor(ct[:c], (c,), k), dtype=torch.int64)
             line[str(N)] = {"ms": round(ms, 3), "encrypts_per_s": round(N / ms * 1e3), "ok": bool(torch.equal(got, m[:c]))}
+            subs = k.crt_keys() if a.crt else None
+            if subs:
+                xs = [torch.empty((N, sk.lc), dtype=torch.int32, device=dev) for sk in subs]
+                cc = torch.empty_like(ct)
+
+                def enc_crt():
+                    for sk, x in zip(subs, xs):
+                        efl.lib.check(lib.efl_pl_fbpowm(*sk.args(), None, x.data_ptr(), N, 7, 0, sh))
+                    efl.lib.check(lib.efl_pl_crt_join(*k.args(), xs[0].data_ptr(), xs[1].data_ptr(), m.data_ptr(),
+                                                      cc.data_ptr(), N, sh))
+                enc_crt()
+                e0.record(st)
+                for _ in range(5):
+                    enc_crt()
+                e1.record(st)
+                e1.synchronize()
+                ms = e0.elapsed_time(e1) / 5
+                line[str(N)].update({"crt_ms": round(ms, 3), "crt_encrypts_per_s": round(N / ms * 1e3),
+                                     "crt_equal": bool(torch.equal(cc, ct)),
+                                     "crt_tables_MiB": round(sum(sk.block.numel() for sk in subs) * 4 / 2**20, 1)})
         print(json.dumps(line), flush=True)
         del kp, k
+        import gc
+        gc.collect()
         torch.cuda.empty_cache()
 
 
