@@ -129,15 +129,31 @@ def _limbs28_rows(vals, L: int, nbytes: int) -> np.ndarray:
 # (tools/table_window_probe.py, profiles/r03/table_window_*.jsonl): the examples' 1024-bit key
 # 53.9 -> 69.6 M encrypts/s from W = 12 to 16 (1.1 GiB table), the reference default 4096-bit key
 # 823 k -> 979 k/s from W = 10 to 12 (1.4 GiB). 1.5 GiB is about half a percent of a 288 GB HBM.
-TABLE_MAX_BYTES = 3 << 29
+# Round 4: 4 GiB per keypair (profiles/r04/table_window_*.jsonl: the 1024-bit key 65.2 -> 76.2 M
+# encrypts/s from W = 16 to 18 (4.0 GiB), 80.8 M/s at W = 20 (14 GiB); the 4096-bit key 0.99 -> 1.07
+# -> 1.14 -> 1.22 -> 1.31 M/s from W = 12 to 16 (1.4 -> 17.7 GiB)). A public-key holder spends it on
+# its one table; the key owner, whose encryptions go by CRT, on the two CRT sub-tables (half each),
+# building its n^2 table only if it is ever walked (KeyBlock.ensure_table). About 1.4 % of a 288 GB
+# HBM; EFL_PL_TABLE_MAX_MIB overrides it.
+TABLE_MAX_BYTES = 4 << 30
+WINDOW_MAX = 24
 
 
-def choose_table_window(a_bits: int, entry_bytes: int, max_bytes: int = TABLE_MAX_BYTES) -> int:
-    """Widest window W <= 16 whose table (ceil(a_bits / W) rows x 2^W - 1 entries of entry_bytes:
-    the n^2 words of every layout the key keeps) fits max_bytes. 2048-bit a of a 4096-bit n (the
-    reference default) -> W = 12, 512-bit a of a 1024-bit n (the examples) -> W = 16."""
+def table_max_bytes() -> int:
+    """The per-keypair table budget: EFL_PL_TABLE_MAX_MIB (MiB) if set, else TABLE_MAX_BYTES."""
+    v = os.environ.get("EFL_PL_TABLE_MAX_MIB", "")
+    return int(v) << 20 if v else TABLE_MAX_BYTES
+
+
+def choose_table_window(a_bits: int, entry_bytes: int, max_bytes: int | None = None) -> int:
+    """Widest window W <= WINDOW_MAX whose table (ceil(a_bits / W) rows x 2^W - 1 entries of
+    entry_bytes: the n^2 words of every layout the key keeps) fits max_bytes (default
+    table_max_bytes()). With 4 GiB: 2048-bit a of a 4096-bit n (the reference default) -> W = 13,
+    512-bit a of a 1024-bit n (the examples) -> W = 18."""
+    if max_bytes is None:
+        max_bytes = table_max_bytes()
     best = 1
-    for W in range(1, 17):
+    for W in range(1, WINDOW_MAX + 1):
         if -(-a_bits // W) * ((1 << W) - 1) * entry_bytes > max_bytes:
             break
         best = W
@@ -327,9 +343,12 @@ class KeyBlock:
     """Host derivation + device upload of every constant the kernels read (efl_pl_key)."""
 
     def __init__(self, n: int, hs: int, a_bits: int, group_size: int, p=None, q=None, device=None,
-                 table_window=None, reuse_table=None, walk_start=None):
+                 table_window=None, reuse_table=None, walk_start=None, max_bytes=None, defer_table=None):
         """walk_start: the fixed-base walk's accumulator starts from walk_start (mod n^2) instead of 1,
-        so efl_pl_fbpowm gives walk_start * hs^(a') mod n^2 (the CRT keys of crt_keys)."""
+        so efl_pl_fbpowm gives walk_start * hs^(a') mod n^2 (the CRT keys of crt_keys). max_bytes:
+        the table's byte budget (default table_max_bytes()). defer_table: build the fixed-base table
+        on its first use (ensure_table) instead of now; None = defer exactly when the key owner's
+        encryption goes by CRT (crt_capable), which never walks this table."""
         if n.bit_length() < 128:
             raise errors.UnimplementedError("n of fewer than 128 bits is not supported on the GPU")
         if p is not None and q is not None and p == q:
@@ -341,6 +360,7 @@ class KeyBlock:
         self.n, self.hs, self.p, self.q = n, hs, p, q
         self.a_bits, self.group_size = a_bits, group_size
         self._window_arg = table_window     # an explicit window also sizes the CRT sub-tables
+        self._max_bytes = table_max_bytes() if max_bytes is None else int(max_bytes)
         need = max(n.bit_length(), 2 * max(p or 0, q or 0).bit_length())
         ln = next((c for c in _LIMB_CLASSES if 32 * c >= need), None)
         if ln is None:
@@ -419,7 +439,7 @@ class KeyBlock:
         # radix-2^28 copy of the table for the sliced family the n^2 kernels use (include/efl_hip.h)
         fam = kernel_slicing(ln, False)
         L28 = limbs28_total(2 * ln, 2 * ln // fam) if fam else 0
-        W = int(table_window) if table_window else choose_table_window(a_bits, 4 * (self.lc + L28))
+        W = int(table_window) if table_window else choose_table_window(a_bits, 4 * (self.lc + L28), self._max_bytes)
         if not 1 <= W <= 24:
             raise errors.InvalidArgumentError("table_window must be in [1, 24]")
         cols = (1 << W) - 1
@@ -445,26 +465,52 @@ class KeyBlock:
                 r28_one = put(R28 % n2, self.lc)          # R28 mod n^2 as 32-bit words (table build)
             else:
                 L28 = 0
-        r_one = d.off_n2_one
         head = torch.from_numpy(np.concatenate(words).view(np.int32)).to(self.device)
-        # the key block without its tables runs the build (n^2 powm / multiply kernels)
-        d.off_table = -1
-        saved = (d.table_rows, d.off_table28)
-        d.table_rows, d.off_table28 = 0, -1
+        # the key block without its tables runs the build (n^2 powm / multiply kernels); until a table
+        # is attached the descriptor says so (table_rows 0: the encryption entry points refuse)
+        self._head = head
+        self._tab = (W, rows, cols, L28, d.off_n2_one, r28_one if L28 else None, walk_start, Rc)
+        d.off_table, d.table_rows, d.off_table28 = -1, 0, -1
         self.block, self.ptr = head, head.data_ptr()
+        self.has_table = False
         src = reuse_table
-        if src is not None and (src.n, src.hs, src.a_bits, src.table_window, src.lc) == (n, hs, a_bits, W, self.lc) \
+        if src is not None and getattr(src, "has_table", False) \
+                and (src.n, src.hs, src.a_bits, src.table_window, src.lc) == (n, hs, a_bits, W, self.lc) \
                 and torch.device(src.device) == torch.device(self.device) \
                 and (src.desc.off_table28 >= 0) == bool(L28) and (not L28 or src.desc.n2_28_len == L28):
             # set_private_key on a key whose public part is unchanged: the tables are the same
             o32, o28 = src.desc.off_table, src.desc.off_table28
-            t32 = src.block[o32:o32 + rows * cols * self.lc]
-            t28 = src.block[o28:o28 + rows * cols * L28] if L28 else None
-        else:
-            t32, t28 = self._build_table(hs % n2, n2, W, rows, cols, head, r_one, r28_one if L28 else None, L28)
-        d.table_rows, d.off_table28 = saved
+            self._attach(src.block[o32:o32 + rows * cols * self.lc],
+                         src.block[o28:o28 + rows * cols * L28] if L28 else None)
+        elif not (self.crt_capable() if defer_table is None else defer_table):
+            self.ensure_table()
+        # the key owner's CRT encryption keys (crt_keys), carried over when only the private part
+        # was set again
+        self._crt = None
+        if src is not None and getattr(src, "_crt", None) and (src.p, src.q) == (self.p, self.q) \
+                and (src.hs, src.a_bits, src.group_size) == (hs, a_bits, group_size) \
+                and torch.device(src.device) == torch.device(self.device):
+            self._crt = src._crt
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def ensure_table(self):
+        """Build and attach the fixed-base table if this key block has none yet (a deferred table:
+        the key owner's, whose own encryptions go by CRT). Returns self."""
+        if not self.has_table:
+            W, rows, cols, L28, r_one, r28_one, _, _ = self._tab
+            t32, t28 = self._build_table(self.hs % (self.n * self.n), self.n * self.n, W, rows, cols, self._head,
+                                         r_one, r28_one, L28)
+            self._attach(t32, t28)
+            torch.cuda.current_stream(self.device).synchronize()
+        return self
+
+    def _attach(self, t32, t28):
+        d = self.desc
+        head = self._head
+        W, rows, cols, L28, _, _, walk_start, Rc = self._tab
+        n2 = self.n * self.n
         parts = [head, t32.reshape(-1)]
-        d.off_table = head.numel()
+        d.table_rows, d.off_table = rows, head.numel()
         if L28:
             d.off_table28 = head.numel() + t32.numel()
             parts.append(t28.reshape(-1))
@@ -477,14 +523,20 @@ class KeyBlock:
                 self.block[d.off_n2_one28:d.off_n2_one28 + L28] = \
                     torch.from_numpy(_limbs28(s0 * (1 << (28 * L28)) % n2, L28).view(np.int32)).to(self.device)
         self.ptr = self.block.data_ptr()
-        # the key owner's CRT encryption keys (crt_keys), carried over when only the private part
-        # was set again
-        self._crt = None
-        if src is not None and getattr(src, "_crt", None) and (src.p, src.q) == (self.p, self.q) \
-                and (src.hs, src.a_bits, src.group_size) == (hs, a_bits, group_size) \
-                and torch.device(src.device) == torch.device(self.device):
-            self._crt = src._crt
-        torch.cuda.current_stream(self.device).synchronize()
+        self.has_table = True
+
+    def crt_capable(self) -> bool:
+        """Whether the key owner's encryption goes by CRT (crt_keys): the private key factors n
+        (p q = n, p != q), half-length primes of a supported limb class, EFL_PL_CRT_ENCRYPT not 0."""
+        if not self.desc.has_private or os.environ.get("EFL_PL_CRT_ENCRYPT", "1") == "0":
+            return False
+        if self.p == self.q or self.p * self.q != self.n:
+            return False
+        for x in (self.p, self.q):
+            ln_x = next((c for c in _LIMB_CLASSES if 32 * c >= x.bit_length()), None)
+            if ln_x is None or 2 * ln_x != self.ln:
+                return False
+        return True
 
     def crt_keys(self):
         """The key owner's encryption keys: (KeyBlock of (p, hs mod p^2), KeyBlock of (q, hs mod
@@ -497,20 +549,18 @@ class KeyBlock:
         still encrypts correctly there (paillier.cc:103-131), and the public-key path keeps that."""
         if self._crt is None:
             self._crt = False
-            if self.desc.has_private and os.environ.get("EFL_PL_CRT_ENCRYPT", "1") != "0" \
-                    and self.p != self.q and self.p * self.q == self.n:
+            if self.crt_capable():
                 subs = []
                 p2, q2 = self.p * self.p, self.q * self.q
                 R = 1 << (32 * self.lc)   # the n^2 Montgomery radix: the join yields hsa R (efl_pl_crt_join)
                 for x, start in ((self.p, R * pow(q2, -1, p2)), (self.q, R * pow(p2, -1, q2))):
-                    ln_x = next((c for c in _LIMB_CLASSES if 32 * c >= x.bit_length()), None)
-                    if ln_x is None or 2 * ln_x != self.ln:
-                        return None
                     # the walk mod p^2 yields hs^(a') R (q^2)^-1, mod q^2 hs^(a') R (p^2)^-1: the join
                     # v = q^2 yp + p^2 yq mod n^2 = hs^(a') R then needs no modular product, and
-                    # g(m) hs^(a') = mont(g(m), v) is one
+                    # g(m) hs^(a') = mont(g(m), v) is one. The two sub-tables share the keypair's
+                    # budget (half each); the key owner's n^2 table is deferred (ensure_table)
                     subs.append(KeyBlock(x, self.hs % (x * x), self.a_bits, self.group_size, device=self.device,
-                                         walk_start=start, table_window=self._window_arg))
+                                         walk_start=start, table_window=self._window_arg,
+                                         max_bytes=self._max_bytes // 2, defer_table=False))
                 self._crt = tuple(subs)
         return self._crt or None
 
@@ -817,6 +867,8 @@ class PaillierKeypair(object):
         if crt is not None:
             out = crt
         else:
+            if hsa_limbs is None:
+                k.ensure_table()          # fresh randomness walks the n^2 table
             _efl_lib.check(_lib.efl_pl_encrypt(*k.args(), m.data_ptr(),
                                                hsa_limbs.data_ptr() if hsa_limbs is not None else None,
                                                out.data_ptr(), N, self.seed, ctr, _stream(k.device)))
@@ -831,6 +883,7 @@ class PaillierKeypair(object):
                 if h is not None:
                     sub[j0:j1] = h
                     continue
+                k.ensure_table()
                 _efl_lib.check(_lib.efl_pl_encrypt(*k.args(), msub[j0:j1].data_ptr(), None, sub[j0:j1].data_ptr(),
                                                    j1 - j0, self.seed, ctr + c0, _stream(k.device)))
             out[idx] = sub
@@ -859,6 +912,7 @@ class PaillierKeypair(object):
         out = self._crt_encrypt(zeros, n, counter_base, a_dev if a is not None else None)
         if out is None:
             out = torch.empty((n, k.lc), dtype=torch.int32, device=k.device)
+            k.ensure_table()
             _efl_lib.check(_lib.efl_pl_fbpowm(*k.args(), a_dev.data_ptr() if a is not None else None,
                                               out.data_ptr(), n, self.seed, counter_base, _stream(k.device)))
         return CipherTensor(out, (n,), k)

@@ -15,6 +15,10 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libefl_hip.so)")
+    # The suite makes hundreds of keypairs; the production per-keypair table budget (4 GiB, e.g. a
+    # 3.8 GB table for a 512-bit test key) would only slow their setup. Tests run with round 3's
+    # 1.5 GiB unless they set the budget themselves (results never depend on the table's window).
+    os.environ.setdefault("EFL_PL_TABLE_MAX_MIB", "1536")
     # build the oracle (CPU checker) and the HIP library if they are missing; an existing library
     # is never rebuilt here (tests/test_abi.py::test_library_built_from_this_tree fails if it is
     # stale), so a GPU run uses exactly the .so that was pushed with the tree

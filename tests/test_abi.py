@@ -135,15 +135,30 @@ def test_product_does_not_import_oracle():
 
 
 def test_table_window_choice():
-    """choose_table_window: the widest window <= 16 whose table (both layouts) fits 1.5 GiB."""
-    from efl.privacy.paillier_cipher import choose_table_window, TABLE_MAX_BYTES, limbs28_total
+    """choose_table_window: the widest window <= WINDOW_MAX whose table (both layouts) fits the
+    per-keypair budget (4 GiB, EFL_PL_TABLE_MAX_MIB overrides); the key owner's CRT sub-tables get
+    half of it each."""
+    from efl.privacy.paillier_cipher import choose_table_window, TABLE_MAX_BYTES, WINDOW_MAX, limbs28_total
     # entry bytes: the n^2 words plus the radix-2^28 copy of the C = 32 family
     entry = {n: 4 * (n // 16 + limbs28_total(n // 16, max(1, n // 16 // 32))) for n in (512, 1024, 2048, 4096)}
-    assert choose_table_window(2048, entry[4096]) == 12   # reference default key: 4096-bit n, 2048-bit a
-    assert choose_table_window(512, entry[1024]) == 16    # the examples' 1024-bit key
-    assert choose_table_window(1024, entry[2048]) == 14
+    B = TABLE_MAX_BYTES        # the production budget (the test session runs with 1.5 GiB, conftest)
+    assert choose_table_window(2048, entry[4096], B) == 13   # reference default key: 4096-bit n, 2048-bit a
+    assert choose_table_window(512, entry[1024], B) == 18    # the examples' 1024-bit key
+    assert choose_table_window(1024, entry[2048], B) == 15
+    assert choose_table_window(2048, entry[2048], TABLE_MAX_BYTES // 2) == 13   # 4096-bit key's sub-tables
+    assert choose_table_window(512, entry[512], TABLE_MAX_BYTES // 2) == 18     # 1024-bit key's sub-tables
+    assert choose_table_window(2048, entry[4096], 3 << 29) == 12                 # round 3's 1.5 GiB
     for a_bits in (1, 7, 64, 256, 513, 1024, 2048, 4096, 8192):
         for eb in entry.values():
-            W = choose_table_window(a_bits, eb)
+            W = choose_table_window(a_bits, eb, B)
             assert W == 1 or -(-a_bits // W) * ((1 << W) - 1) * eb <= TABLE_MAX_BYTES
-            assert W == 16 or -(-a_bits // (W + 1)) * ((1 << (W + 1)) - 1) * eb > TABLE_MAX_BYTES
+            assert W == WINDOW_MAX or -(-a_bits // (W + 1)) * ((1 << (W + 1)) - 1) * eb > TABLE_MAX_BYTES
+
+
+def test_table_budget_env(monkeypatch):
+    from efl.privacy import paillier_cipher as pc
+    monkeypatch.setenv("EFL_PL_TABLE_MAX_MIB", "1536")
+    assert pc.table_max_bytes() == 3 << 29
+    monkeypatch.delenv("EFL_PL_TABLE_MAX_MIB")
+    assert pc.table_max_bytes() == pc.TABLE_MAX_BYTES
+    assert pc.choose_table_window(2048, 2208) == 13          # default budget when unset

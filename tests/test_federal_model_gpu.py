@@ -163,8 +163,10 @@ def test_key_rotation_every_two_steps():
         assert np.allclose(y, x @ qdp(W0) + x @ w0, rtol=1e-4, atol=1e-4), step
         assert np.allclose((W1 + w1) - (W0 + w0), -LR * x.T @ qdp(dy), rtol=1e-4, atol=2e-5), step
     for side in (send, recv):
-        key_bytes = side[2]["key_bytes"]
-        assert key_bytes > 1 << 20                       # the fixed-base table dominates (MiB scale)
+        # the fixed-base tables dominate (MiB scale): the receiver's n^2 table, the key owner's two
+        # CRT sub-tables (its n^2 table is never walked, so never built)
+        key_bytes = side[2]["key_bytes"] + side[2]["crt_bytes"]
+        assert key_bytes > 1 << 20
         # right after the re-keys of steps 2 and 4 the same bytes are live: nothing of the old key
         # stays behind (a leak would add at least one key block)
         assert abs(side[4]["m1"] - side[2]["m1"]) < key_bytes // 4, [r["m1"] for r in side]

@@ -183,6 +183,33 @@ def test_crt_not_used_for_private_key_not_factoring_n(efl):
                                                    p2, p2)
 
 
+def test_owner_table_deferred_until_walked(efl):
+    """The key owner's encryptions go by CRT, so its n^2 fixed-base table is built only when the
+    public-key path is asked for (crt_encrypt = False here): the raw ABI refuses the walk before
+    that (no table, no fault), and both paths give the same ciphertexts after it."""
+    from efl.privacy import paillier_cipher as pc
+    k = CRT_KEYS[0]
+    kp = keypair(efl, k, seed=21)
+    key = kp.key
+    assert not key.has_table and key.crt_capable()
+    m = torch.tensor([3, -4, 2**40, 0], dtype=torch.int64)
+    crt = kp.encrypt(m, counter_base=5).tensor.to_hex().strings()
+    assert not key.has_table                                   # CRT needs only the sub-tables
+    subs = key.crt_keys()
+    budget = pc.table_max_bytes()
+    assert all(sk.block.numel() * 4 <= budget // 2 + (64 << 20) for sk in subs)
+    ct = torch.empty((4, key.lc), dtype=torch.int32, device="cuda")
+    md = m.cuda()
+    rc = pc._lib.efl_pl_encrypt(*key.args(), md.data_ptr(), None, ct.data_ptr(), 4, 21, 5, None)
+    assert rc != 0                                             # ABORTED: no fixed-base table yet
+    kp.crt_encrypt = False
+    pub = kp.encrypt(m, counter_base=5).tensor.to_hex().strings()
+    assert key.has_table and pub == crt
+    assert pc._lib.efl_pl_encrypt(*key.args(), md.data_ptr(), None, ct.data_ptr(), 4, 21, 5, None) == 0
+    # a public-key holder builds its table at once
+    assert keypair(efl, k, private=False).key.has_table
+
+
 def test_crt_keys_survive_set_private_key(efl):
     k = CRT_KEYS[0]
     kp = keypair(efl, k)

@@ -158,18 +158,19 @@ def test_table_built_on_gpu_matches_host(efl):
 
 
 @pytest.mark.parametrize("k", ALL, ids=ids)
-def test_default_table_window_keeps_the_radix28_table(efl, k):
-    """The default window (the widest whose table, both layouts, fits 1.5 GiB) never drops the
-    radix-2^28 copy the n^2 kernels walk: a window one wider at 4096-bit n would exceed its 1 GiB cap
-    and fall back to the 32-bit-limb encryption, at half the speed (profiles/r03/table_window_*)."""
+def test_default_table_window_keeps_the_radix28_table(efl, k, monkeypatch):
+    """The default window (the widest whose table, both layouts, fits the 4 GiB budget) keeps the
+    radix-2^28 copy the n^2 kernels walk (profiles/r04/table_window_*)."""
     from efl.privacy import paillier_cipher as pc
+    monkeypatch.delenv("EFL_PL_TABLE_MAX_MIB", raising=False)     # the production budget
     n, hs = int(k["n"], 16), int(k["hs"], 16)
     kb = pc.KeyBlock(n, hs, k["a_bits"], 1)
-    want = {512: 16, 1024: 16, 2048: 14, 4096: 12}[8 * k["n_bytes"]]
+    assert kb.has_table
+    want = {512: 20, 1024: 18, 2048: 15, 4096: 13}[8 * k["n_bytes"]]
     assert kb.table_window == want
     if pc.kernel_slicing(kb.ln, False):
         assert kb.desc.off_table28 >= 0
-    assert kb.block.numel() * 4 <= pc.TABLE_MAX_BYTES + (64 << 20)   # the table plus the key's constants
+    assert kb.block.numel() * 4 <= pc.table_max_bytes() + (64 << 20)   # the table plus the key's constants
 
 
 @pytest.mark.parametrize("k,c", fams(ALL))

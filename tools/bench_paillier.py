@@ -47,7 +47,7 @@ for n_bytes, g in keys:
     kp = efl.paillier.Keypair(seed=7)
     kp.set_keys_ints(n, hs, n_bytes // 2, g, p, q, n_bytes)
     setup = time.perf_counter() - t0
-    k = kp.key
+    k = kp.key.ensure_table()   # the owner's n^2 table is deferred (KeyBlock)
     N = N_4096 if k.ln >= 128 else N_SMALL
     m = torch.randint(-2**40, 2**40, (N,), dtype=torch.int64, device=dev)
     out = torch.empty((N, k.lc), dtype=torch.int32, device=dev)

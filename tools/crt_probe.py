@@ -34,7 +34,7 @@ def main():
         n, hs, p, q = pc.generate_keypair_ints(n_bytes, 24, random.Random(n_bytes))
         kp = efl.paillier.Keypair(seed=7)
         kp.set_keys_ints(n, hs, a_bytes, g, p, q, n_bytes)
-        k = kp.key
+        k = kp.key.ensure_table()   # the owner's n^2 table is deferred (KeyBlock)
         subs = k.crt_keys()
         m = torch.randint(-2**40, 2**40, (N,), dtype=torch.int64, device=dev)
         ct = torch.empty((N, k.lc), dtype=torch.int32, device=dev)

@@ -30,7 +30,7 @@ def main():
     n, hs, p, q = pc.generate_keypair_ints(n_bytes, 24, random.Random(n_bytes))
     kp = efl.paillier.Keypair(seed=7)
     kp.set_keys_ints(n, hs, a_bytes, g, p, q, n_bytes)
-    k = kp.key
+    k = kp.key.ensure_table()   # the owner's n^2 table is deferred (KeyBlock)
     u, v, w = bench.STAGE_P_MATMUL
     gen = torch.Generator(device=dev).manual_seed(3)
     x = torch.randn(u, v, device=dev, generator=gen)

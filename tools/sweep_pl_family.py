@@ -32,7 +32,7 @@ for n_bytes, a_bytes, g, N, fams in KEYS:
         pc.set_kernel_slicing(ln, False, C)
         kp = efl.paillier.Keypair(seed=5)
         kp.set_keys_ints(n, hs, a_bytes, g, None, None, n_bytes)
-        k = kp.key
+        k = kp.key.ensure_table()   # the owner's n^2 table is deferred (KeyBlock)
         m = torch.randint(-2**40, 2**40, (N,), dtype=torch.int64, device=dev)
         ct = torch.empty((N, k.lc), dtype=torch.int32, device=dev)
 

@@ -38,7 +38,7 @@ def main():
     n, hs, p, q = pc.generate_keypair_ints(n_bytes, 24, random.Random(n_bytes))
     kp = efl.paillier.Keypair(seed=7)
     kp.set_keys_ints(n, hs, n_bytes // 2, 10 if n_bytes == 128 else 1, p, q, n_bytes)
-    k = kp.key
+    k = kp.key.ensure_table()   # the owner's n^2 table is deferred (KeyBlock)
     subs = k.crt_keys()
     out = {"tool": "walk_probe", "library": efl.lib.LIB_PATH.rsplit("/", 1)[-1], "version": efl.lib.version(),
            "n_bits": 8 * n_bytes, "table_window": k.table_window}
