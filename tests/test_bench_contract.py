@@ -1,0 +1,66 @@
+"""The BENCH line's contract (the driver parses bench.py's one JSON line), checked on the line the
+final round-4 build printed on the MI355X box (profiles/r04/bench.json) and on the code that makes
+it: every required key, the roofline and cpu_baseline objects, and their internal consistency."""
+import json
+import os
+
+from conftest import ROOT
+
+REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+            "scaling", "vs_baseline", "dtype", "data", "config"}
+
+
+def _line():
+    with open(os.path.join(ROOT, "profiles", "r04", "bench.json")) as f:
+        lines = [ln for ln in f.read().splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    return json.loads(lines[0])
+
+
+def test_bench_line_has_the_contract_keys():
+    d = _line()
+    assert REQUIRED <= set(d)
+    with open(os.path.join(ROOT, "BASELINE.json")) as f:
+        base = json.load(f)
+    assert d["metric"] == base["metric"] and d["unit"] == "GiB/s"
+    assert d["higher_is_better"] is True and d["scaling"] == "weak" and d["vs_baseline"] is None
+    assert d["n_gpus"] == 1 and "workload" in d["config"] and "model" not in d["config"]
+    # value = N x 0.25 GiB per step / step time
+    assert abs(d["value"] - 0.25 * d["n_gpus"] / (d["ms_per_step"] * 1e-3)) / d["value"] < 0.01
+
+
+def test_roofline_object():
+    r = _line()["roofline"]
+    assert {"bound", "achieved", "peak", "unit", "frac", "traffic"} <= set(r)
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    # algorithmic bytes per launch (20 B/elem x 64 Mi) / kernel time = achieved
+    assert r["algorithmic_bytes_per_launch"] == 20 * 65536 * 1024
+    # PMC traffic within 0.1 % of the algorithmic bytes: no wasted re-reads
+    assert abs(r["traffic"] / r["algorithmic_bytes_per_launch"] - 1) < 1e-3
+
+
+def test_cpu_baseline_object():
+    c = _line()["cpu_baseline"]
+    assert {"value", "unit", "cores", "kind", "sample"} <= set(c)
+    assert c["kind"] in ("port", "reference") and c["cores"] >= 1 and c["unit"] == "GiB/s"
+
+
+def test_config3_both_layouts_reported():
+    c3 = _line()["config3"]
+    assert c3["roundtrip_ok"] and c3["views"]["roundtrip_ok"]
+    assert c3["table_entries"] == {"encode": 4096, "decode": 4096}
+    assert c3["views"]["table_entries"] == {"encode": 1, "decode": 1}
+
+
+def test_pmc_traffic_names_the_shipping_library():
+    """profiles/pmc_traffic.json (bench.py's roofline.traffic source) was measured with the library
+    this tree builds (efl_version's source hash), so the bench line's traffic_source and library
+    agree."""
+    import subprocess
+    with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+        tr = json.load(f)
+    h = subprocess.check_output(["make", "-s", "-C", os.path.join(ROOT, "elastic-federated-learning-solution_amd"),
+                                 "src-hash"], text=True).strip()
+    assert tr["library"].endswith("src " + h), (tr["library"], h)
+    assert tr["elements"] == 65536 * 1024
