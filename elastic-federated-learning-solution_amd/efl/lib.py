@@ -350,6 +350,14 @@ class BatchTables:
 
     def __init__(self, srcs, d0s, d1s, coalesce="single"):
         dev = srcs[0].device
+        if len(srcs) != len(d0s) or len(srcs) != len(d1s):
+            raise errors.InvalidArgumentError("batched tables: as many entries in every stream")
+        for i, (s, a, b) in enumerate(zip(srcs, d0s, d1s)):
+            # the kernels read each entry as numel() contiguous elements from its data pointer
+            if not (s.is_contiguous() and a.is_contiguous() and b.is_contiguous()):
+                raise errors.InvalidArgumentError(f"batched tables: entry {i} is not contiguous")
+            if a.numel() != s.numel() or b.numel() != s.numel():
+                raise errors.InvalidArgumentError(f"batched tables: entry {i} has streams of different sizes")
         self.keep = (srcs, d0s, d1s)
         runs = None
         if coalesce:

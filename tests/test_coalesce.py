@@ -57,3 +57,19 @@ def test_empty_entries_are_dropped():
     runs = coalesce_runs([xs[0], e, xs[1], xs[2]], [ms[0], e.long(), ms[1], ms[2]], [es[0], e.long(), es[1], es[2]])
     assert [r[3] for r in runs] == [30]
     assert coalesce_runs([e], [e.long()], [e.long()]) == []
+
+
+def test_batch_tables_reject_strided_and_mismatched_entries():
+    """BatchTables checks its entries on the host before any device table exists: a strided view
+    or streams of different sizes are refused (the kernels read numel() contiguous elements)."""
+    import pytest
+    from efl import errors
+    from efl.lib import BatchTables
+    x = torch.empty(10, 4)
+    m = torch.empty(10, 4, dtype=torch.int64)
+    with pytest.raises(errors.InvalidArgumentError, match="not contiguous"):
+        BatchTables([x[:, ::2]], [m[:, ::2].contiguous()], [m[:, ::2].contiguous()])
+    with pytest.raises(errors.InvalidArgumentError, match="different sizes"):
+        BatchTables([x], [m[:5]], [m])
+    with pytest.raises(errors.InvalidArgumentError, match="as many"):
+        BatchTables([x, x], [m], [m])

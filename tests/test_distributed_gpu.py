@@ -1,4 +1,4 @@
-"""GPU, world_size 2: the multi-GPU layout of §8(e) run with the HIP kernels under two ranks.
+"""GPU, world sizes 2 and 4: the multi-GPU layout of §8(e) run with the HIP kernels under several ranks.
 
 The driver's 1-GPU box cannot host two RCCL ranks (RCCL refuses two ranks on one device), so both
 ranks share cuda:0 over gloo (efl.distributed.choose_backend) — the same code path an 8-GPU node
@@ -73,7 +73,8 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_two_ranks_share_cuda0_bit_identical():
+@pytest.mark.parametrize("world", [2, 4])
+def test_ranks_share_cuda0_bit_identical(world):
     import efl
     from oracle import fxp
     with socket.socket() as sk:
@@ -81,7 +82,7 @@ def test_two_ranks_share_cuda0_bit_identical():
         port = sk.getsockname()[1]
     ctx = tmp.get_context("spawn")
     q = ctx.Queue()
-    procs = tmp.start_processes(_worker, args=(2, port, q), nprocs=2, join=False, start_method="spawn")
+    procs = tmp.start_processes(_worker, args=(world, port, q), nprocs=world, join=False, start_method="spawn")
     try:
         parts = q.get(timeout=100)
     except Exception:
@@ -89,8 +90,10 @@ def test_two_ranks_share_cuda0_bit_identical():
         raise
     while not procs.join(timeout=30):
         pass
-    assert [p["backend"] for p in parts] == ["gloo", "gloo"]
-    assert [(p["s"], p["e"]) for p in parts] == [(0, parts[1]["s"]), (parts[0]["e"], N_F)]
+    assert [p["backend"] for p in parts] == ["gloo"] * world
+    # contiguous shards that tile [0, N_F) in rank order
+    assert parts[0]["s"] == 0 and parts[-1]["e"] == N_F
+    assert all(parts[r]["e"] == parts[r + 1]["s"] for r in range(world - 1))
 
     x, m = _plain()
     Mg = np.concatenate([p["M"] for p in parts])
@@ -116,9 +119,9 @@ def test_two_ranks_share_cuda0_bit_identical():
     kp1, rng1 = edist.shard_keypair(seed, pk, N_P, 1, 0, private_key={"p": k["p"], "q": k["q"]})
     assert rng1 == (0, N_P)
     whole = kp1.encrypt(m)
-    cg = parts[0]["ct"] + parts[1]["ct"]
+    cg = [c for p in parts for c in p["ct"]]
     assert cg == whole.tensor.to_hex().strings()
-    assert [p["counter"] for p in parts] == [parts[0]["pe"], N_P]
+    assert [p["counter"] for p in parts] == [p["pe"] for p in parts] and parts[-1]["pe"] == N_P
     assert torch.equal(kp1.decrypt(efl.HexTensor.from_strings(cg), dtype=torch.int64).cpu(), m)
 
 
