@@ -14,6 +14,8 @@ run() {
     pltests) timeout -k 10 900 python -u -m pytest tests/test_paillier_gpu.py tests/test_paillier_crt_gpu.py \
               tests/test_federal_model_gpu.py tests/test_paillier_reference_cases_gpu.py tests/test_paillier_layer_gpu.py \
               -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r04_pltests.log 2>&1 ;;
+    dist)   timeout -k 10 600 python -u -m pytest tests/test_distributed_gpu.py tests/test_bench_launcher.py tests/test_fxp_gpu.py \
+              -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r04_dist.log 2>&1 ;;
     smoke)  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r04_smoke.log 2>&1 ;;
     bench)  timeout -k 10 400 python -u bench.py > gpurun_out/r04_bench.json 2> gpurun_out/r04_bench.err ;;
     bench2) timeout -k 10 300 python -u bench.py --gpus 2 --steps 20 --warmup 3 --no-extras --no-cpu-baseline \
