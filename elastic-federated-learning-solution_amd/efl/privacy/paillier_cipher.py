@@ -1011,6 +1011,10 @@ class PaillierKeypair(object):
         if ym.shape[0] != v:
             raise errors.InvalidArgumentError("the size of x's 1st dim should be equal to the size of y's 2nd dim.")
         w = ym.shape[1]
+        if u and v and w:
+            rx = torch.stack([xe.max() - xe.min(), ye.max() - ye.min()]).tolist()
+            if rx[0] + rx[1] > MATMUL_MAX_SPREAD:
+                return self._matmul_composed(x, xe, ym, ye)
         zpos = torch.empty((u * w, k.lc), dtype=torch.int32, device=k.device)
         zneg = torch.empty_like(zpos)
         ze = torch.empty((u, w), dtype=torch.int64, device=k.device)
@@ -1023,9 +1027,44 @@ class PaillierKeypair(object):
             return CipherTensor(z.limbs, (u, w), k), ze
         return CipherTensor(zpos, (u, w), k), ze
 
+    def _matmul_composed(self, x, xe, ym, ye):
+        """PaillierMatmul term by term, as the reference forms it (paillier.cc:1008-1034): term (i, j, k)
+        = x_ij^y_jk (PaillierMulScalar; x^-1 for y < 0) shifted by 2^(xe_ij + ye_jk - m_ik), m_ik the
+        minimum over j, and the terms of an output multiplied mod n^2. Used when the exponents spread
+        past MATMUL_MAX_SPREAD: the shifts then run through _exp2_chunked's bounded launches. The
+        product is exact, so the ciphertexts equal efl_pl_matmul's; rows go in chunks of about
+        256 MiB of terms."""
+        k = self.key
+        u, v = x.shape
+        w = ym.shape[1]
+        rows = max(1, (256 << 20) // (v * w * k.lc * 4))
+        zs, ms = [], []
+        for i0 in range(0, u, rows):
+            i1 = min(u, i0 + rows)
+            r = i1 - i0
+            xr = CipherTensor(x.limbs[i0 * v:i1 * v], (r, v, 1), k)
+            t = self.mul_scalar(xr, ym.reshape(1, v, w))                          # [r, v, w]
+            s = xe[i0:i1].reshape(r, v, 1) + ye.reshape(1, v, w)
+            m = s.amin(dim=1)                                                      # [r, w]
+            t = self._exp2_chunked(t.limbs, (s - m.reshape(r, 1, w)).reshape(-1).contiguous())
+            t = t.view(r, v, w, k.lc)
+            while t.shape[1] > 1:                                                  # product over j
+                h = t.shape[1] // 2
+                a = t[:, :h].contiguous()
+                b = t[:, h:2 * h].contiguous()
+                p = torch.empty_like(a)
+                _efl_lib.check(_lib.efl_pl_add(*k.args(), a.data_ptr(), b.data_ptr(), p.data_ptr(),
+                                               r * h * w, _stream(k.device)))
+                t = torch.cat([p, t[:, 2 * h:]], dim=1) if t.shape[1] % 2 else p
+            zs.append(t.reshape(r * w, k.lc))
+            ms.append(m)
+        return CipherTensor(torch.cat(zs).contiguous(), (u, w), k), torch.cat(ms)
+
     def mul_exp2(self, x, exp):
         """PaillierMulExp2 (paillier.cc:680-751): z = x^(2^y) mod n^2, y int32/int64 >= 0, y
-        squarings per element on the GPU (efl_pl_mul_exp2). x and y broadcast first (paillier.py:87-91)."""
+        squarings per element on the GPU (efl_pl_mul_exp2). x and y broadcast first (paillier.py:87-91).
+        A launch squares at most MAX_SHIFT times per element; longer shifts are cut into launches of
+        at most that many (_exp2_chunked), so any y >= 0 is computed as the reference computes it."""
         k = self.key
         x = self._cipher(x)
         y = _scalar_operand(exp, k.device)
@@ -1034,14 +1073,40 @@ class PaillierKeypair(object):
         shape = _broadcast_shape(x.shape, y.shape)
         x = _expand(x, shape)
         y = y.expand(shape).reshape(-1).contiguous()
-        out = torch.empty_like(x.limbs)
-        bad = torch.empty(1, dtype=torch.int64, device=k.device)
-        _efl_lib.check(_lib.efl_pl_mul_exp2(*k.args(), x.limbs.data_ptr(), y.data_ptr(), out.data_ptr(), x.numel(),
-                                            bad.data_ptr(), _stream(k.device)))
-        b = int(bad.item())
+        out, b = self._exp2_launch(x.limbs, y)
         if b >= 0:
-            _raise_shift(int(y[b].item()))
+            if int(y[b].item()) < 0:
+                raise errors.InvalidArgumentError("y should be a positive tensor.")
+            out = self._exp2_chunked(x.limbs, y)
         return CipherTensor(out, shape, k)
+
+    def _exp2_launch(self, limbs, y):
+        """One efl_pl_mul_exp2 launch: (out, index of the first element with y < 0 or y > MAX_SHIFT,
+        or -1)."""
+        k = self.key
+        out = torch.empty_like(limbs)
+        bad = torch.empty(1, dtype=torch.int64, device=k.device)
+        _efl_lib.check(_lib.efl_pl_mul_exp2(*k.args(), limbs.data_ptr(), y.data_ptr(), out.data_ptr(),
+                                            limbs.shape[0], bad.data_ptr(), _stream(k.device)))
+        return out, int(bad.item())
+
+    def _exp2_chunked(self, limbs, y):
+        """x^(2^y) for shifts past one launch's MAX_SHIFT squarings: x^(2^(a + b)) = (x^(2^a))^(2^b),
+        so each launch squares every element min(remaining, MAX_SHIFT) times (0 = the element passes
+        through) until no element has squarings left. Like the reference's y squarings
+        (paillier.cc:728-731) the work grows with y; each launch stays bounded."""
+        if bool((y < 0).any()):
+            raise errors.InvalidArgumentError("y should be a positive tensor.")
+        rem = y.clone()
+        cur = limbs
+        while True:
+            step = torch.clamp(rem, max=_SHIFT_CHUNK)
+            cur, b = self._exp2_launch(cur, step)
+            if b >= 0:   # cannot happen: every step is within [0, MAX_SHIFT]
+                raise errors.InternalError(f"shift chunk of element {b} refused")
+            rem -= step
+            if not bool((rem > 0).any()):
+                return cur
 
     def shift_add(self, x, x_exponent, y, y_exponent):
         """The ciphertext half of FixedPointTensor.__add__ (paillier.py:119-132):
@@ -1061,19 +1126,25 @@ class PaillierKeypair(object):
         _efl_lib.check(_lib.efl_pl_fxp_add(*k.args(), x.limbs.data_ptr(), xe.data_ptr(), y.limbs.data_ptr(),
                                            ye.data_ptr(), out.data_ptr(), x.numel(), bad.data_ptr(), _stream(k.device)))
         b = int(bad.item())
+        m = torch.minimum(xe, ye)
         if b >= 0:
-            _raise_shift(abs(int(xe[b].item()) - int(ye[b].item())))
-        return CipherTensor(out, shape, k), torch.minimum(xe, ye).reshape(shape)
+            # a shift past one launch's squarings: the reference's own composition (two
+            # PaillierMulExp2, one PaillierAdd), the shifts cut into bounded launches
+            xs = self._exp2_chunked(x.limbs, xe - m)
+            ys = self._exp2_chunked(y.limbs, ye - m)
+            out = torch.empty_like(xs)
+            _efl_lib.check(_lib.efl_pl_add(*k.args(), xs.data_ptr(), ys.data_ptr(), out.data_ptr(), x.numel(),
+                                           _stream(k.device)))
+        return CipherTensor(out, shape, k), m.reshape(shape)
 
 
-MAX_SHIFT = 1 << 16   # pl_common.h kMaxShift
+MAX_SHIFT = 1 << 16   # pl_common.h kMaxShift: squarings per element in one launch
+_SHIFT_CHUNK = MAX_SHIFT   # squarings per launch of _exp2_chunked (tests lower it; never above MAX_SHIFT)
+# PaillierMatmul: an exponent spread (max - min of x_exponent plus that of y_exponent) past this
+# runs as the reference's per-term composition (_matmul_composed) instead of one efl_pl_matmul,
+# whose bit-level loop would spend that many squarings per output in one launch
+MATMUL_MAX_SPREAD = MAX_SHIFT
 
-
-def _raise_shift(y: int):
-    if y < 0:
-        raise errors.InvalidArgumentError("y should be a positive tensor.")
-    raise errors.UnimplementedError(f"shift by 2^{y}: more than {MAX_SHIFT} squarings per element are not "
-                                    "supported on the GPU (DESIGN.md §5)")
 
 
 def _scalar_operand(s, device):
