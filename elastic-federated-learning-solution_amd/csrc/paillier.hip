@@ -1025,8 +1025,8 @@ __global__ __launch_bounds__(256) void k_to_int64(const uint32_t* __restrict__ m
 inline bool key_ok(const efl_pl_key* d, bool need_private, int ln_max) {
   if (!d) { set_error("null key descriptor"); return false; }
   if (d->a_bits <= 0 || d->a_bits > 8192) { set_error("a_bits must be in [1, 8192]"); return false; }
-  if (d->ln != 16 && d->ln != 32 && d->ln != 64 && d->ln != 128) {
-    set_error("unsupported limb count %d (n of 512/1024/2048/4096 bits)", d->ln);
+  if (d->ln != 16 && d->ln != 32 && d->ln != 64 && d->ln != 128 && d->ln != 256) {
+    set_error("unsupported limb count %d (n of 512/1024/2048/4096/8192 bits)", d->ln);
     return false;
   }
   if (d->ln > ln_max) {
@@ -1055,15 +1055,17 @@ inline int table_ok(const efl_pl_key* d) {
 }
 
 // kernel family per key size: 0 = one lane per element (paillier.hip), C = sliced over 2ln/C (n^2
-// ops) or ln/C (decryption) lanes of C limbs (paillier_sliced.hip). [ln 16/32/64/128][n^2 ops, decrypt]
+// ops) or ln/C (decryption) lanes of C limbs (paillier_sliced.hip). [ln 16/32/64/128/256][n^2 ops, decrypt]
 // measured: decryption profiles/r01/bench_pl*.jsonl; n^2 ops profiles/r02/sweep_pl_family.jsonl — with
 // the round-2 table window, 32 limbs per lane is the fastest encryption at every key size (512-bit
 // 1.7x, 1024-bit 1.06x incl. the MNIST matmul, 2048-bit 1.14x, 4096-bit 1.51x the round-1 choice)
-constexpr int kDefaultSlicing[4][2] = {{32, 8}, {32, 32}, {32, 32}, {32, 32}};
-int g_slicing[4][2] = {{32, 8}, {32, 32}, {32, 32}, {32, 32}};
-inline int ln_index(int ln) { return ln == 16 ? 0 : ln == 32 ? 1 : ln == 64 ? 2 : 3; }
+// 8192-bit n (round 4): n^2 ops over 16 lanes of 32 limbs, decryption over 8 (the 4096-bit key's
+// n^2 family), both without a one-lane alternative
+constexpr int kDefaultSlicing[5][2] = {{32, 8}, {32, 32}, {32, 32}, {32, 32}, {32, 32}};
+int g_slicing[5][2] = {{32, 8}, {32, 32}, {32, 32}, {32, 32}, {32, 32}};
+inline int ln_index(int ln) { return ln == 16 ? 0 : ln == 32 ? 1 : ln == 64 ? 2 : ln == 128 ? 3 : 4; }
 inline int slicing(int ln, int dec) { return g_slicing[ln_index(ln)][dec]; }
-bool g_slicing_set[4][2] = {};   // set explicitly through efl_pl_tune: used as given for every size
+bool g_slicing_set[5][2] = {};   // set explicitly through efl_pl_tune: used as given for every size
 
 // Decryption family for n elements: the default (C = 32) unless the launch would give fewer than
 // 768 waves (3 per 4 SIMDs) of that family; then C = 8 (four times the lanes per element). Round 3
@@ -1137,8 +1139,9 @@ struct RunPowm {
 template <int LN>
 hipError_t run_invert(Key k, const uint32_t* x, uint32_t* out, long long N, unsigned long long* bad, hipStream_t s,
                       const void* sel = nullptr, int sel_kind = 0) {
-  // four LDS numbers per lane: 32 lanes per workgroup for n^2 of 8192 bits (128 KiB)
-  constexpr int block = LN >= 128 ? 32 : kPlBlock;
+  // four LDS numbers per lane: 32 lanes per workgroup for n^2 of 8192 bits (128 KiB), 16 for n^2
+  // of 16384 bits (128 KiB)
+  constexpr int block = LN >= 256 ? 16 : LN >= 128 ? 32 : kPlBlock;
   constexpr bool reg = 2 * LN <= 64;   // u, v in registers (k_invert)
   const size_t lds = (size_t)(reg ? 2 : 4) * (2 * LN) * block * 4;
   hipLaunchKernelGGL((k_invert<LN, reg>), dim3((unsigned)((N + block - 1) / block)), dim3(block), lds, s, k, x, out,
@@ -1152,7 +1155,8 @@ hipError_t invert_ln(Key k, const uint32_t* x, uint32_t* out, long long N, unsig
     case 16: return run_invert<16>(k, x, out, N, bad, s, sel, sel_kind);
     case 32: return run_invert<32>(k, x, out, N, bad, s, sel, sel_kind);
     case 64: return run_invert<64>(k, x, out, N, bad, s, sel, sel_kind);
-    default: return run_invert<128>(k, x, out, N, bad, s, sel, sel_kind);
+    case 128: return run_invert<128>(k, x, out, N, bad, s, sel, sel_kind);
+    default: return run_invert<256>(k, x, out, N, bad, s, sel, sel_kind);
   }
 }
 
@@ -1186,7 +1190,7 @@ using namespace efl;
 EFL_API int efl_pl_encrypt(const void* key_block, const efl_pl_key* key, const int64_t* plaintext,
                            const uint32_t* hsa, uint32_t* ciphertext, int64_t n, uint64_t seed,
                            int64_t counter_base, void* stream) {
-  if (!key_ok(key, false, 128)) return EFL_E_INVALID_ARGUMENT;
+  if (!key_ok(key, false, 256)) return EFL_E_INVALID_ARGUMENT;
   if (n < 0) { set_error("negative count"); return EFL_E_INVALID_ARGUMENT; }
   if (n == 0) return EFL_OK;
   if (!hsa) {
@@ -1204,7 +1208,7 @@ EFL_API int efl_pl_encrypt(const void* key_block, const efl_pl_key* key, const i
 
 EFL_API int efl_pl_fbpowm(const void* key_block, const efl_pl_key* key, const uint32_t* a, uint32_t* hsa,
                           int64_t n, uint64_t seed, int64_t counter_base, void* stream) {
-  if (!key_ok(key, false, 128)) return EFL_E_INVALID_ARGUMENT;
+  if (!key_ok(key, false, 256)) return EFL_E_INVALID_ARGUMENT;
   if (n <= 0) return n < 0 ? EFL_E_INVALID_ARGUMENT : EFL_OK;
   const int rc = table_ok(key);
   if (rc != EFL_OK) return rc;
@@ -1218,7 +1222,7 @@ EFL_API int efl_pl_fbpowm(const void* key_block, const efl_pl_key* key, const ui
 
 EFL_API int efl_pl_crt_join(const void* key_block, const efl_pl_key* key, const uint32_t* xp, const uint32_t* xq,
                             const int64_t* plaintext, uint32_t* z, int64_t n, void* stream) {
-  if (!key_ok(key, true, 128)) return key && !key->has_private ? EFL_E_ABORTED : EFL_E_INVALID_ARGUMENT;
+  if (!key_ok(key, true, 256)) return key && !key->has_private ? EFL_E_ABORTED : EFL_E_INVALID_ARGUMENT;
   if (n <= 0) return n < 0 ? EFL_E_INVALID_ARGUMENT : EFL_OK;
   Key k{(const uint32_t*)key_block, *key};
   hipStream_t s = (hipStream_t)stream;
@@ -1228,7 +1232,8 @@ EFL_API int efl_pl_crt_join(const void* key_block, const efl_pl_key* key, const 
     case 16: hipLaunchKernelGGL((k_crt_join<16>), dim3(g), dim3(kPlBlock), lds, s, k, xp, xq, z, (long long)n); break;
     case 32: hipLaunchKernelGGL((k_crt_join<32>), dim3(g), dim3(kPlBlock), lds, s, k, xp, xq, z, (long long)n); break;
     case 64: hipLaunchKernelGGL((k_crt_join<64>), dim3(g), dim3(kPlBlock), lds, s, k, xp, xq, z, (long long)n); break;
-    default: hipLaunchKernelGGL((k_crt_join<128>), dim3(g), dim3(kPlBlock), lds, s, k, xp, xq, z, (long long)n); break;
+    case 128: hipLaunchKernelGGL((k_crt_join<128>), dim3(g), dim3(kPlBlock), lds, s, k, xp, xq, z, (long long)n); break;
+    default: hipLaunchKernelGGL((k_crt_join<256>), dim3(g), dim3(kPlBlock), lds, s, k, xp, xq, z, (long long)n); break;
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !plaintext) return hip_status(e, "efl_pl_crt_join");
@@ -1243,7 +1248,7 @@ EFL_API int efl_pl_crt_join(const void* key_block, const efl_pl_key* key, const 
 
 EFL_API int efl_pl_decrypt(const void* key_block, const efl_pl_key* key, const uint32_t* ciphertext,
                            uint32_t* magnitude, int8_t* negative, int64_t n, void* stream) {
-  if (!key_ok(key, true, 128)) return key && !key->has_private ? EFL_E_ABORTED : EFL_E_INVALID_ARGUMENT;
+  if (!key_ok(key, true, 256)) return key && !key->has_private ? EFL_E_ABORTED : EFL_E_INVALID_ARGUMENT;
   if (n < 0) { set_error("negative count"); return EFL_E_INVALID_ARGUMENT; }
   if (n == 0) return EFL_OK;
   Key k{(const uint32_t*)key_block, *key};
@@ -1255,14 +1260,15 @@ EFL_API int efl_pl_decrypt(const void* key_block, const efl_pl_key* key, const u
     case 16: e = run_decrypt<16>(k, ciphertext, magnitude, (signed char*)negative, n, s); break;
     case 32: e = run_decrypt<32>(k, ciphertext, magnitude, (signed char*)negative, n, s); break;
     case 64: e = run_decrypt<64>(k, ciphertext, magnitude, (signed char*)negative, n, s); break;
-    default: e = run_decrypt<128>(k, ciphertext, magnitude, (signed char*)negative, n, s); break;
+    case 128: e = run_decrypt<128>(k, ciphertext, magnitude, (signed char*)negative, n, s); break;
+    default: set_error("no one-lane decryption for p^2 of %d bits", 32 * key->ln); return EFL_E_INVALID_ARGUMENT;
   }
   return hip_status(e, "efl_pl_decrypt");
 }
 
 EFL_API int efl_pl_add(const void* key_block, const efl_pl_key* key, const uint32_t* x, const uint32_t* y,
                        uint32_t* z, int64_t n, void* stream) {
-  if (!key_ok(key, false, 128)) return EFL_E_INVALID_ARGUMENT;
+  if (!key_ok(key, false, 256)) return EFL_E_INVALID_ARGUMENT;
   if (n <= 0) return n < 0 ? EFL_E_INVALID_ARGUMENT : EFL_OK;
   Key k{(const uint32_t*)key_block, *key};
   const int C = slicing(key->ln, 0);
@@ -1273,7 +1279,7 @@ EFL_API int efl_pl_add(const void* key_block, const efl_pl_key* key, const uint3
 
 EFL_API int efl_pl_powm(const void* key_block, const efl_pl_key* key, const uint32_t* x, const uint32_t* exps,
                         int exp_words, uint32_t* z, int64_t n, void* stream) {
-  if (!key_ok(key, false, 128)) return EFL_E_INVALID_ARGUMENT;
+  if (!key_ok(key, false, 256)) return EFL_E_INVALID_ARGUMENT;
   if (exp_words <= 0) { set_error("exp_words must be positive"); return EFL_E_INVALID_ARGUMENT; }
   if (n <= 0) return n < 0 ? EFL_E_INVALID_ARGUMENT : EFL_OK;
   Key k{(const uint32_t*)key_block, *key};
@@ -1314,7 +1320,7 @@ hipError_t powm_family<pl::ExpWords>(Key k, const uint32_t* x, pl::ExpWords xs, 
 
 // common prologue of the ops with a device status word: argument checks, bad <- -1
 int status_prologue(const efl_pl_key* key, int64_t n, int64_t* bad, hipStream_t s, const char* op) {
-  if (!key_ok(key, false, 128)) return EFL_E_INVALID_ARGUMENT;
+  if (!key_ok(key, false, 256)) return EFL_E_INVALID_ARGUMENT;
   if (!bad) { set_error("%s: null status word", op); return EFL_E_INVALID_ARGUMENT; }
   if (n < 0) { set_error("%s: negative count", op); return EFL_E_INVALID_ARGUMENT; }
   return hip_status(hipMemsetAsync(bad, 0xFF, sizeof(int64_t), s), op);
@@ -1389,7 +1395,7 @@ EFL_API int efl_pl_fxp_add(const void* key_block, const efl_pl_key* key, const u
 
 EFL_API int efl_pl_invert(const void* key_block, const efl_pl_key* key, const uint32_t* x, uint32_t* z,
                           int64_t n, int64_t* bad, void* stream) {
-  if (!key_ok(key, false, 128)) return EFL_E_INVALID_ARGUMENT;
+  if (!key_ok(key, false, 256)) return EFL_E_INVALID_ARGUMENT;
   if (!bad) { set_error("null status word"); return EFL_E_INVALID_ARGUMENT; }
   hipStream_t s = (hipStream_t)stream;
   hipError_t e = hipMemsetAsync(bad, 0xFF, sizeof(int64_t), s);
@@ -1400,7 +1406,8 @@ EFL_API int efl_pl_invert(const void* key_block, const efl_pl_key* key, const ui
     case 16: e = run_invert<16>(k, x, z, (long long)n, b, s); break;
     case 32: e = run_invert<32>(k, x, z, (long long)n, b, s); break;
     case 64: e = run_invert<64>(k, x, z, (long long)n, b, s); break;
-    default: e = run_invert<128>(k, x, z, (long long)n, b, s); break;
+    case 128: e = run_invert<128>(k, x, z, (long long)n, b, s); break;
+    default: e = run_invert<256>(k, x, z, (long long)n, b, s); break;
   }
   return hip_status(e, "efl_pl_invert");
 }
@@ -1409,7 +1416,7 @@ EFL_API int efl_pl_matmul(const void* key_block, const efl_pl_key* key, const ui
                           const int64_t* x_exponent, const int64_t* y_mantissa, const int64_t* y_exponent,
                           uint32_t* z_pos, uint32_t* z_neg, int64_t* z_exponent, int u, int v, int w,
                           void* stream) {
-  if (!key_ok(key, false, 128)) return EFL_E_INVALID_ARGUMENT;
+  if (!key_ok(key, false, 256)) return EFL_E_INVALID_ARGUMENT;
   if (u < 0 || v <= 0 || w < 0) { set_error("bad matmul shape"); return EFL_E_INVALID_ARGUMENT; }
   if ((long long)u * w == 0) return EFL_OK;
   Key k{(const uint32_t*)key_block, *key};
@@ -1426,7 +1433,7 @@ EFL_API int efl_pl_matmul(const void* key_block, const efl_pl_key* key, const ui
 }
 
 EFL_API int efl_pl_tune(int ln, int decrypt, int limbs_per_lane) {
-  if (ln != 16 && ln != 32 && ln != 64 && ln != 128) { set_error("unsupported limb count %d", ln); return EFL_E_INVALID_ARGUMENT; }
+  if (ln != 16 && ln != 32 && ln != 64 && ln != 128 && ln != 256) { set_error("unsupported limb count %d", ln); return EFL_E_INVALID_ARGUMENT; }
   if (decrypt == 2) {   // sliced decryption's exponentiation: 1 sliding window (default), 0 binary
     if (limbs_per_lane < 0) return pl::sl_dec_window(-1);
     if (limbs_per_lane > 1) { set_error("decryption method must be 0 (binary) or 1 (window)"); return EFL_E_INVALID_ARGUMENT; }
@@ -1447,6 +1454,7 @@ EFL_API int efl_pl_tune(int ln, int decrypt, int limbs_per_lane) {
   if (limbs_per_lane < 0) return slicing(ln, dec);   // query
   if (limbs_per_lane == 0) {
     if (!dec && ln > 64) { set_error("no one-lane kernels for n^2 of %d bits", 64 * ln); return EFL_E_INVALID_ARGUMENT; }
+    if (dec && ln > 128) { set_error("no one-lane decryption for p^2 of %d bits", 32 * ln); return EFL_E_INVALID_ARGUMENT; }
   } else if (!pl::sliced_available(dec ? ln : 2 * ln, limbs_per_lane)) {
     set_error("no sliced kernels with %d limbs per lane for %d-limb moduli", limbs_per_lane, dec ? ln : 2 * ln);
     return EFL_E_INVALID_ARGUMENT;

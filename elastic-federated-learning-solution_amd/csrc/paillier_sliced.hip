@@ -1431,7 +1431,8 @@ hipError_t run_decrypt(const Key& k, const uint32_t* ct, uint32_t* mag, signed c
 bool sliced_available(int L, int C) {
   switch (L * 1000 + C) {
     case 16008: case 32008: case 64008: case 128008: case 256008:
-    case 32016: case 32032: case 64016: case 64032: case 128016: case 128032: case 256016: case 256032: return true;
+    case 32016: case 32032: case 64016: case 64032: case 128016: case 128032: case 256016: case 256032:
+    case 512032: return true;
     default: return false;
   }
 }
@@ -1451,6 +1452,7 @@ bool sliced_available(int L, int C) {
     case 128032: { constexpr int CC = 32, GG = 4; return EXPR; } \
     case 256016: { constexpr int CC = 16, GG = 16; return EXPR; } \
     case 256032: { constexpr int CC = 32, GG = 8; return EXPR; } \
+    case 512032: { constexpr int CC = 32, GG = 16; return EXPR; } \
     default: return hipErrorInvalidValue;                    \
   }
 

@@ -102,9 +102,9 @@ def reset_kernel_slicing(ln: int, decrypt: bool) -> int:
 
 # kernel families compiled per key size (ln): n^2 ops, decryption
 SLICINGS = {16: ([0, 8, 16, 32], [0, 8]), 32: ([0, 8, 16, 32], [0, 8, 16, 32]), 64: ([0, 8, 16, 32], [0, 8, 16, 32]),
-            128: ([8, 16, 32], [0, 8, 16, 32])}
+            128: ([8, 16, 32], [0, 8, 16, 32]), 256: ([32], [8, 16, 32])}
 
-_LIMB_CLASSES = (16, 32, 64, 128)
+_LIMB_CLASSES = (16, 32, 64, 128, 256)
 MAX_TABLE_BITS = 1 << 40      # gmp_utils.h:20 FBPOWM_MAX_TABLE_MEM, compared against entries x bits
 # above this the radix-2^28 copy of the fixed-base table is not built (a table chosen under
 # TABLE_MAX_BYTES always has it; an explicit table_window up to 24 may ask for more)
@@ -364,7 +364,7 @@ class KeyBlock:
         need = max(n.bit_length(), 2 * max(p or 0, q or 0).bit_length())
         ln = next((c for c in _LIMB_CLASSES if 32 * c >= need), None)
         if ln is None:
-            raise errors.UnimplementedError(f"n of {n.bit_length()} bits: at most 4096 supported")
+            raise errors.UnimplementedError(f"n of {n.bit_length()} bits: at most 8192 supported")
         self.ln, self.lc, self.lh = ln, 2 * ln, ln // 2
         if a_bits <= 0 or a_bits > 8192:
             raise errors.InvalidArgumentError("a_bytes must be in [1, 1024]")

@@ -202,7 +202,8 @@ typedef struct {
  * = (1 + |m| n)^(sign) * hsa mod n^2. hsa: [n][2*ln] limbs, or NULL for the reference's
  * hsa == "0" case: a fresh a of a_bits bits per element from Philox4x32-10(key = seed, counter =
  * counter_base + i) and hsa = hs^(a') through the fixed-base table (a' = a with every
- * group_size-bit group bit-reversed, as mpz_fbpowm does). n of up to 4096 bits.
+ * group_size-bit group bit-reversed, as mpz_fbpowm does). n of up to 8192 bits (ln 16/32/64/128/256; a
+ * smaller n runs in the smallest class that holds it, zero-padded).
  */
 int efl_pl_encrypt(const void* key_block, const efl_pl_key* key, const int64_t* plaintext,
                    const uint32_t* hsa, uint32_t* ciphertext, int64_t n, uint64_t seed,
@@ -228,7 +229,7 @@ int efl_pl_crt_join(const void* key_block, const efl_pl_key* key, const uint32_t
 /*
  * PaillierDecrypt (paillier.cc:505-561, _Decrypt :296-312): CRT decryption of [n][2*ln]
  * ciphertexts into |m| ([n][ln] limbs) and negative[i] = (m < 0) where m > ceil(2n/3) maps to
- * m - n. ABORTED "No private key." without p, q. n of up to 4096 bits. The sliced kernels take a
+ * m - n. ABORTED "No private key." without p, q. n of up to 8192 bits. The sliced kernels take a
  * stream-ordered scratch slab for the sliding-window exponentiation (efl_pl_tune decrypt = 2); a
  * failed allocation returns the HIP error.
  */
@@ -293,10 +294,11 @@ int efl_pl_matmul(const void* key_block, const efl_pl_key* key, const uint32_t* 
                   uint32_t* z_pos, uint32_t* z_neg, int64_t* z_exponent, int u, int v, int w,
                   void* stream);
 
-/* Kernel family for keys of ln limbs (16/32/64/128): decrypt = 0 selects the n^2 ops (encrypt,
+/* Kernel family for keys of ln limbs (16/32/64/128/256): decrypt = 0 selects the n^2 ops (encrypt,
  * fbpowm, add, powm, matmul), 1 decryption. limbs_per_lane 0 = one lane per element (n^2 ops:
- * ln <= 64 only), 16 or 32 = one number spread over L/limbs_per_lane lanes (L = 2 ln, or ln for
- * decryption); -1 queries; -2 restores the default. Returns the previous choice, or a negative
+ * ln <= 64 only; decryption: ln <= 128), 8, 16 or 32 = one number spread over L/limbs_per_lane lanes
+ * (L = 2 ln, or ln for decryption; ln = 256: n^2 ops 32 only); -1 queries; -2 restores the
+ * default. Returns the previous choice, or a negative
  * error code. Results are identical across families; only speed differs. With the default
  * (never set, or restored by -2) a decryption of too few elements to give every SIMD a wave takes
  * more lanes per element; a family set explicitly is used for every size. decrypt = 2 selects the

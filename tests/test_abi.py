@@ -162,3 +162,22 @@ def test_table_budget_env(monkeypatch):
     monkeypatch.delenv("EFL_PL_TABLE_MAX_MIB")
     assert pc.table_max_bytes() == pc.TABLE_MAX_BYTES
     assert pc.choose_table_window(2048, 2208) == 13          # default budget when unset
+
+def test_kernel_families_per_key_class():
+    """efl_pl_tune's family table (host logic, no GPU): every limb class up to 8192-bit n has its
+    measured default, the 8192-bit key's n^2 ops run over 16 lanes of 32 limbs and its decryption
+    over 8, with no one-lane kernels for either; 16384-bit n is refused. KeyBlock refuses n past
+    8192 bits before it touches the device."""
+    import efl
+    from efl.privacy import paillier_cipher as pc
+    lib = efl.lib.raw()
+    for ln, (ops, dec) in pc.SLICINGS.items():
+        assert lib.efl_pl_tune(ln, 0, -1) in ops and lib.efl_pl_tune(ln, 1, -1) in dec
+    assert lib.efl_pl_tune(256, 0, -1) == 32 and lib.efl_pl_tune(256, 1, -1) == 32
+    assert lib.efl_pl_tune(256, 0, 0) == -3 and "one-lane" in lib.efl_last_error().decode()
+    assert lib.efl_pl_tune(256, 1, 0) == -3 and "one-lane" in lib.efl_last_error().decode()
+    assert lib.efl_pl_tune(256, 0, 16) == -3          # no 32-lane n^2 family compiled
+    assert lib.efl_pl_tune(512, 0, -1) == -3
+    n = (1 << 8200) + 1
+    with pytest.raises(efl.errors.UnimplementedError, match="at most 8192"):
+        pc.KeyBlock(n, 2, 1024, 1)

@@ -23,7 +23,7 @@ ENC_KEYS = [k for k in KAT["keys"] if k["n_bytes"] <= 128]
 ALL = KAT["keys"]
 # kernel families per ln (mirrors paillier_cipher.SLICINGS): (n^2 ops, decryption)
 SLICINGS = {16: ([0, 8, 16, 32], [0, 8]), 32: ([0, 8, 16, 32], [0, 8, 16, 32]), 64: ([0, 8, 16, 32], [0, 8, 16, 32]),
-            128: ([8, 16, 32], [0, 8, 16, 32])}
+            128: ([8, 16, 32], [0, 8, 16, 32]), 256: ([32], [8, 16, 32])}
 
 
 def fams(keys, decrypt=False):

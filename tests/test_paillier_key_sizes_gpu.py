@@ -1,10 +1,11 @@
-"""Key sizes between the compiled limb classes. The reference takes any n_bytes
+"""Key sizes between and past the round-3 limb classes. The reference takes any n_bytes
 (GeneratePaillierKeypair, paillier.cc:799-913: primes of n_bytes * 4 bits); the build runs a key in
-the smallest limb class that holds n and p^2 (512 / 1024 / 2048 / 4096-bit n: KeyBlock's
+the smallest limb class that holds n and p^2 (512 / 1024 / 2048 / 4096 / 8192-bit n: KeyBlock's
 _LIMB_CLASSES), the numbers zero-padded to it, so 768-, 1000-, 1536- and 3072-bit keys (3072 bits is
 the usual 128-bit security level) run in the 1024-, 1024-, 2048- and 4096-bit kernels. Montgomery
 arithmetic only needs the modulus below R, so the results must be the oracle's bit for bit: fresh
-randomness encryption by the public path and by CRT, decryption, the homomorphic ops and matmul."""
+randomness encryption by the public path and by CRT, decryption, the homomorphic ops and matmul.
+8192-bit keys (round 4) run their n^2 ops over 16 lanes per number and decrypt over 8."""
 import random
 
 import numpy as np
@@ -17,7 +18,7 @@ from oracle import philox
 pytestmark = pytest.mark.gpu
 
 # (n_bytes, limb class of n)
-SIZES = [(96, 32), (125, 32), (192, 64), (384, 128)]
+SIZES = [(96, 32), (125, 32), (192, 64), (384, 128), (1024, 256)]
 
 
 @pytest.fixture(scope="module")
