@@ -173,6 +173,19 @@ def _limbs28(x: int, L: int) -> np.ndarray:
     return np.array([(x >> (28 * k)) & 0xFFFFFFF for k in range(L)], dtype="<u4")
 
 
+def table_passes(W: int, cols: int):
+    """The table build's doubling passes (KeyBlock._build_table): pass k computes the columns
+    (0-based) lo .. lo + cnt - 1, lo = 2^k, as column i times b^(2^k) for i in 0 .. cnt - 1, so column
+    c holds b^(c + 1) and every source column was made by an earlier pass."""
+    out = []
+    for k in range(W):
+        lo = 1 << k
+        if cols <= lo:
+            break
+        out.append((lo, min(lo, cols - lo)))
+    return out
+
+
 def limbs28_total(ln: int, G: int) -> int:
     """Limbs of the radix-2^28 form the sliced kernels use for an ln-word modulus over G lanes
     (s28::limbs_per_lane(ln, G) * G: R = 2^(28 L) > 4 m)."""
@@ -462,14 +475,13 @@ class KeyBlock:
                 d.off_n2_r2_28 = pos[0]
                 words.append(_limbs28(R28 * R28 % n2, L28))
                 pos[0] += L28
-                r28_one = put(R28 % n2, self.lc)          # R28 mod n^2 as 32-bit words (table build)
             else:
                 L28 = 0
         head = torch.from_numpy(np.concatenate(words).view(np.int32)).to(self.device)
         # the key block without its tables runs the build (n^2 powm / multiply kernels); until a table
         # is attached the descriptor says so (table_rows 0: the encryption entry points refuse)
         self._head = head
-        self._tab = (W, rows, cols, L28, d.off_n2_one, r28_one if L28 else None, walk_start, Rc)
+        self._tab = (W, rows, cols, L28, d.off_n2_one, walk_start, Rc)
         d.off_table, d.table_rows, d.off_table28 = -1, 0, -1
         self.block, self.ptr = head, head.data_ptr()
         self.has_table = False
@@ -497,9 +509,9 @@ class KeyBlock:
         """Build and attach the fixed-base table if this key block has none yet (a deferred table:
         the key owner's, whose own encryptions go by CRT). Returns self."""
         if not self.has_table:
-            W, rows, cols, L28, r_one, r28_one, _, _ = self._tab
+            W, rows, cols, L28, r_one, _, _ = self._tab
             t32, t28 = self._build_table(self.hs % (self.n * self.n), self.n * self.n, W, rows, cols, self._head,
-                                         r_one, r28_one, L28)
+                                         r_one, L28)
             self._attach(t32, t28)
             torch.cuda.current_stream(self.device).synchronize()
         return self
@@ -507,7 +519,7 @@ class KeyBlock:
     def _attach(self, t32, t28):
         d = self.desc
         head = self._head
-        W, rows, cols, L28, _, _, walk_start, Rc = self._tab
+        W, rows, cols, L28, _, walk_start, Rc = self._tab
         n2 = self.n * self.n
         parts = [head, t32.reshape(-1)]
         d.table_rows, d.off_table = rows, head.numel()
@@ -564,51 +576,68 @@ class KeyBlock:
                 self._crt = tuple(subs)
         return self._crt or None
 
-    def _build_table(self, hs, n2, W, rows, cols, head, r_one, r28_one, L28, chunk_entries=1 << 16):
+    def _build_table(self, hs, n2, W, rows, cols, head, r_one, L28, chunk_bytes=64 << 20):
         """T[i][j-1] = hs^(j 2^(W i)) mod n^2 for j in 1..2^W-1, in Montgomery form (x R mod n^2,
         [rows, cols, 2 ln] words) and, with L28, radix-2^28 Montgomery form (x R28 mod n^2,
-        [rows, cols, L28] limbs). Row bases hs^(2^(W i)) come from W squarings each on the host;
-        every entry is then one short GPU exponentiation base_i^j (efl_pl_powm, W-bit exponents)
-        and one GPU product by R (or R28) mod n^2 (efl_pl_add) — the work the reference does with
-        mpz_mul per entry when a keypair is set (gmp_utils.cc:73-88). The row bases come from one
-        native host call (efl_host_sqr_chain: 0.38 s of CPython pow for the 4096-bit key's 170 x 12
-        squarings mod n^2)."""
+        [rows, cols, L28] limbs): the table the reference fills with one mpz_mul per entry when a
+        keypair is set (gmp_utils.cc:73-88), built here with one GPU product per entry as well.
+        One native host call gives every hs^(2^t), t < W rows (efl_host_sqr_chain): P[i][k] =
+        b_i^(2^k) for the row base b_i = hs^(2^(W i)). Column 1 is b_i R; pass k then fills columns
+        2^k + 1 .. 2^(k+1) of every row at once as column i times P[i][k] (efl_pl_add, which
+        multiplies mod n^2: x R * y = x y R), so W passes of independent products replace a chain
+        per row. Round 3 ran an efl_pl_powm of b_i^j per entry (about 1.5 W products each). The
+        radix-2^28 copy is x R times R28 R^-1 (one more product) cut into 28-bit limbs. Launches
+        move at most chunk_bytes of entries."""
         dev, lc = self.device, self.lc
         sh = _stream(dev)
-        # hs^(2^(W i)) for every row: W squarings per row, on the host in native code
-        bases_d = torch.from_numpy(host_sqr_chain(hs, W, rows, n2, lc).view(np.int32)).to(dev)
-        t32 = torch.empty((rows, cols, lc), dtype=torch.int32, device=dev)
-        t28 = torch.empty((rows, cols, L28), dtype=torch.int32, device=dev) if L28 else None
-        exps = torch.arange(1, cols + 1, dtype=torch.int32, device=dev)
-        rows_per = max(1, chunk_entries // cols)
         d = self.desc
-        one = head[r_one:r_one + lc]
-        one28 = head[r28_one:r28_one + lc] if L28 else None
-        if L28:
-            q, r = divmod(np.arange(L28) * 28, 32)
-            qi = torch.from_numpy(q).to(dev)
-            rs = torch.from_numpy(r).to(dev)
-        for r0 in range(0, rows, rows_per):
-            r1 = min(rows, r0 + rows_per)
-            N = (r1 - r0) * cols
-            X = bases_d[r0:r1].unsqueeze(1).expand(r1 - r0, cols, lc).reshape(N, lc).contiguous()
-            E = exps.repeat(r1 - r0).reshape(N, 1).contiguous()
-            T = torch.empty_like(X)
-            _efl_lib.check(_lib.efl_pl_powm(head.data_ptr(), ctypes.byref(d), X.data_ptr(), E.data_ptr(), 1,
-                                            T.data_ptr(), N, sh))
-            Y = one.expand(N, lc).contiguous()
-            _efl_lib.check(_lib.efl_pl_add(head.data_ptr(), ctypes.byref(d), T.data_ptr(), Y.data_ptr(),
-                                           t32[r0:r1].data_ptr(), N, sh))
-            if L28:
-                Y.copy_(one28.expand(N, lc))
-                _efl_lib.check(_lib.efl_pl_add(head.data_ptr(), ctypes.byref(d), T.data_ptr(), Y.data_ptr(),
-                                               X.data_ptr(), N, sh))
-                # x R28 mod n^2 < 2^(32 lc): words past lc (up to the last limb's + 1) are zero
-                pad = int(q.max()) + 2 - lc
-                w = torch.cat([X.to(torch.int64) & 0xFFFFFFFF,
-                               torch.zeros((N, max(1, pad)), dtype=torch.int64, device=dev)], dim=1)
-                limbs = ((w[:, qi] >> rs) | (w[:, qi + 1] << (32 - rs))) & 0xFFFFFFF
-                t28[r0:r1] = limbs.to(torch.int32).reshape(r1 - r0, cols, L28)
+        ptr, dp = head.data_ptr(), ctypes.byref(d)
+
+        def mul(dst, a, b, N):
+            _efl_lib.check(_lib.efl_pl_add(ptr, dp, a.data_ptr(), b.data_ptr(), dst.data_ptr(), N, sh))
+
+        P = torch.from_numpy(host_sqr_chain(hs, 1, rows * W, n2, lc).view(np.int32)).to(dev).reshape(rows, W, lc)
+        t32 = torch.empty((rows, cols, lc), dtype=torch.int32, device=dev)
+        ce = max(1, chunk_bytes // (4 * lc))              # entries per launch
+        col = torch.empty((rows, lc), dtype=torch.int32, device=dev)
+        mul(col, P[:, 0].contiguous(), head[r_one:r_one + lc].expand(rows, lc).contiguous(), rows)
+        t32[:, 0] = col
+        for k, (lo, cnt) in enumerate(table_passes(W, cols)):
+            if cnt >= ce:                                 # long rows: slices of one row, in place
+                for r in range(rows):
+                    for c0 in range(0, cnt, ce):
+                        c1 = min(cnt, c0 + ce)
+                        m = P[r, k].expand(c1 - c0, lc).contiguous()
+                        mul(t32[r, lo + c0:lo + c1], t32[r, c0:c1], m, c1 - c0)
+            else:                                         # short rows: several rows per launch
+                rb = max(1, ce // cnt)
+                for r0 in range(0, rows, rb):
+                    r1 = min(rows, r0 + rb)
+                    src = t32[r0:r1, :cnt].contiguous()
+                    m = P[r0:r1, k:k + 1].expand(r1 - r0, cnt, lc).contiguous()
+                    out = torch.empty_like(src)
+                    mul(out, src, m, (r1 - r0) * cnt)
+                    t32[r0:r1, lo:lo + cnt] = out
+        if not L28:
+            return t32, None
+        t28 = torch.empty((rows, cols, L28), dtype=torch.int32, device=dev)
+        R, R28 = 1 << (32 * lc), 1 << (28 * L28)
+        c28 = torch.from_numpy(_limbs(R28 * pow(R, -1, n2) % n2, lc).view(np.int32)).to(dev)
+        q, r = divmod(np.arange(L28) * 28, 32)
+        qi = torch.from_numpy(q).to(dev)
+        rs = torch.from_numpy(r).to(dev)
+        pad = int(q.max()) + 2 - lc                       # x R28 mod n^2 < 2^(32 lc): words past lc are 0
+        flat32, flat28 = t32.reshape(-1, lc), t28.reshape(-1, L28)
+        total = rows * cols
+        ce28 = max(1, ce // 4)                            # the int64 staging below is 4x the entries
+        for e0 in range(0, total, ce28):
+            e1 = min(total, e0 + ce28)
+            N = e1 - e0
+            X = torch.empty((N, lc), dtype=torch.int32, device=dev)
+            mul(X, flat32[e0:e1], c28.expand(N, lc).contiguous(), N)
+            w = torch.cat([X.to(torch.int64) & 0xFFFFFFFF,
+                           torch.zeros((N, max(1, pad)), dtype=torch.int64, device=dev)], dim=1)
+            flat28[e0:e1] = (((w[:, qi] >> rs) | (w[:, qi + 1] << (32 - rs))) & 0xFFFFFFF).to(torch.int32)
         return t32, t28
 
     def args(self):

@@ -181,3 +181,19 @@ def test_kernel_families_per_key_class():
     n = (1 << 8200) + 1
     with pytest.raises(efl.errors.UnimplementedError, match="at most 8192"):
         pc.KeyBlock(n, 2, 1024, 1)
+
+
+def test_table_build_passes_cover_every_column_once():
+    """KeyBlock._build_table's doubling schedule (host logic): starting from column 0 = b, the
+    passes give column c the power b^(c + 1) for every c < 2^W - 1, each column written once and
+    only from columns written before."""
+    from efl.privacy.paillier_cipher import table_passes
+    for W in range(1, 19):
+        cols = (1 << W) - 1
+        power = [1] + [0] * (cols - 1)
+        for k, (lo, cnt) in enumerate(table_passes(W, cols)):
+            assert lo == 1 << k and 0 < cnt <= lo
+            for i in range(cnt):
+                assert power[i] and not power[lo + i]
+                power[lo + i] = power[i] + lo          # b^(i+1) * b^(2^k)
+        assert power == list(range(1, cols + 1)), W

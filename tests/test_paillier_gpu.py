@@ -130,31 +130,49 @@ def test_fbpowm_kat_any_table_window(efl, k, c, W):
         assert ct.tensor.to_hex().strings() == want
 
 
-def test_table_built_on_gpu_matches_host(efl):
-    """The fixed-base table efl builds on the GPU (row bases on the host, entries base^j by
-    efl_pl_powm, then x R and x R28 by efl_pl_add) equals hs^(j 2^(W i)) R mod n^2 computed with
-    Python ints, in both layouts."""
+def _host_table(hs, n2, W, rows, cols, R):
+    """[rows][cols] of hs^(j 2^(W i)) R mod n^2 with Python ints."""
+    out = []
+    for i in range(rows):
+        b = pow(hs, 1 << (W * i), n2)
+        x, row = 1, []
+        for _ in range(cols):
+            x = x * b % n2
+            row.append(x * R % n2)
+        out.append(row)
+    return out
+
+
+def _as_ints(words, width, bits):
+    w = np.asarray(words, dtype=np.uint32).reshape(-1, width)
+    return [sum(int(v) << (bits * t) for t, v in enumerate(r)) for r in w]
+
+
+@pytest.mark.parametrize("W", [1, 2, 5, 7])
+def test_table_built_on_gpu_matches_host(efl, W):
+    """The fixed-base table efl builds on the GPU (every hs^(2^t) on the host, then column 1 = b R
+    and W passes of one efl_pl_add product per entry, then x R28 by one more) equals
+    hs^(j 2^(W i)) R mod n^2 computed with Python ints, every entry of both layouts; and so does a
+    build whose launches take 8 entries (the per-row path of the long passes)."""
     from efl.privacy import paillier_cipher as pc
     k = ENC_KEYS[1]
     n, hs = int(k["n"], 16), int(k["hs"], 16)
-    kb = pc.KeyBlock(n, hs, k["a_bits"], 1, table_window=5)
+    kb = pc.KeyBlock(n, hs, k["a_bits"], 1, table_window=W)
     d = kb.desc
     n2 = n * n
-    R = 1 << (32 * kb.lc)
+    rows, cols, lc = d.table_rows, d.table_cols, kb.lc
+    want = [v for row in _host_table(hs, n2, W, rows, cols, 1 << (32 * lc)) for v in row]
     blk = kb.block.cpu().numpy().view(np.uint32)
-    rng = np.random.default_rng(2)
-    for _ in range(40):
-        i, j = int(rng.integers(0, d.table_rows)), int(rng.integers(1, d.table_cols + 1))
-        want = pow(hs, j << (5 * i), n2)
-        off = d.off_table + (i * d.table_cols + j - 1) * kb.lc
-        got = int.from_bytes(blk[off:off + kb.lc].tobytes(), "little")
-        assert got == want * R % n2, (i, j)
-        if d.off_table28 >= 0:
-            L28 = d.n2_28_len
-            off = d.off_table28 + (i * d.table_cols + j - 1) * L28
-            limbs = blk[off:off + L28]
-            got28 = sum(int(v) << (28 * t) for t, v in enumerate(limbs))
-            assert got28 == want * (1 << (28 * L28)) % n2, (i, j)
+    assert _as_ints(blk[d.off_table:d.off_table + rows * cols * lc], lc, 32) == want
+    L28 = d.n2_28_len if d.off_table28 >= 0 else 0
+    assert L28
+    inv = pow(1 << (32 * lc), -1, n2) * (1 << (28 * L28))
+    want28 = [v * inv % n2 for v in want]
+    assert _as_ints(blk[d.off_table28:d.off_table28 + rows * cols * L28], L28, 28) == want28
+    W_, rows_, cols_, L28_, r_one, _, _ = kb._tab
+    t32, t28 = kb._build_table(hs % n2, n2, W_, rows_, cols_, kb._head, r_one, L28_, chunk_bytes=8 * 4 * lc)
+    assert torch.equal(t32.reshape(-1), kb.block[d.off_table:d.off_table + rows * cols * lc])
+    assert torch.equal(t28.reshape(-1), kb.block[d.off_table28:d.off_table28 + rows * cols * L28])
 
 
 @pytest.mark.parametrize("k", ALL, ids=ids)
