@@ -226,6 +226,13 @@ __global__ __launch_bounds__(kSlBlock) SL_OCC void k_fbpowm(Key k, const uint32_
 
 // hs^(a') mod n^2 through the radix-2^28 table (same lookup order as fbpowm_mont), result in
 // NORMAL form as this lane's C 32-bit words. Scratch: B (entry / conversion, L28 words per element).
+// Waves per SIMD the one-lane (G = 1) walk kernels are compiled for (build knob for A/B): with the
+// entry and the product-scanning multiply in registers (s28::mul_fips1) the walk takes about 200
+// VGPRs at 2 waves
+#ifndef EFL_WALK1_WAVES
+#define EFL_WALK1_WAVES 2
+#endif
+
 template <int C, int G>
 __device__ __forceinline__ void fbpowm28_walk(uint32_t (&acc)[s28::limbs_per_lane(C * G, G)], const Key& k,
                                               uint32_t* A, uint32_t* B, int E, int words,
@@ -245,11 +252,19 @@ __device__ __forceinline__ void fbpowm28_walk(uint32_t (&acc)[s28::limbs_per_lan
 #else
       const uint32_t* ent = table + ((int64_t)row * cols + (idx - 1)) * L28 + g * C28;
 #endif
+      if constexpr (G == 1 && EFL_MUL_FIPS) {
+        // one lane holds the whole number: the entry goes straight into registers (round 4)
+        uint32_t b[C28];
 #pragma unroll
-      for (int j = 0; j < C28; ++j) B[(g * C28 + j) * E] = ent[j];
-      lds_sync();
-      s28::mont_mul<C28, G>(acc, LdsElem{B, E}, m28, minv28, g);
-      lds_sync();
+        for (int j = 0; j < C28; ++j) b[j] = ent[j];
+        s28::mul_fips1<C28>(acc, b, m28, minv28);
+      } else {
+#pragma unroll
+        for (int j = 0; j < C28; ++j) B[(g * C28 + j) * E] = ent[j];
+        lds_sync();
+        s28::mont_mul<C28, G>(acc, LdsElem{B, E}, m28, minv28, g);
+        lds_sync();
+      }
     }
   }
 }
@@ -273,7 +288,7 @@ __device__ __forceinline__ void fbpowm28(uint32_t (&out)[C], const Key& k, uint3
 }
 
 template <int C, int G>
-__global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_fbpowm28(Key k, const uint32_t* __restrict__ a_in,
+__global__ __launch_bounds__(kSlBlock, C >= 32 ? (G == 1 ? EFL_WALK1_WAVES : 2) : EFL_DEC_WAVES) void k_fbpowm28(Key k, const uint32_t* __restrict__ a_in,
                                                                          uint32_t* __restrict__ out, long long N,
                                                                          uint64_t seed, long long ctr0) {
   constexpr int L = C * G, E = kSlBlock / G;
@@ -403,7 +418,7 @@ __device__ __forceinline__ void store_from_mont28(uint32_t* out, uint32_t (&t)[s
 // (tools/isa_loops.py) and only its code placement moved — keeping the round-1 tail there in the
 // same build measured slower still (-3 %).
 template <int C, int G>
-__global__ __launch_bounds__(kSlBlock, C >= 32 ? 2 : EFL_DEC_WAVES) void k_encrypt28(Key k, const long long* __restrict__ m,
+__global__ __launch_bounds__(kSlBlock, C >= 32 ? (G == 1 ? EFL_WALK1_WAVES : 2) : EFL_DEC_WAVES) void k_encrypt28(Key k, const long long* __restrict__ m,
                                                                           uint32_t* __restrict__ out, long long N,
                                                                           uint64_t seed, long long ctr0) {
   constexpr int L = C * G, E = kSlBlock / G;
@@ -1116,6 +1131,8 @@ __device__ __forceinline__ void m_func(uint32_t (&res)[C / 2], const uint32_t* _
       load28<C28>(ent, slot + (size_t)(v >> 1) * G * CP);   // in flight during the squarings
 #pragma unroll 1
       for (int t = b; t >= j; --t) s28::mont_sqr<C28, G>(a, SCR, E, m28, minv28, g);
+      // (mul_fips1 here, for one-lane numbers, measured 3 % slower: the 1024-bit decryption's 256
+      // VGPRs were already full, round 4)
       to_lds<C28>(BASE, E, g, ent);
       lds_sync();
       s28::mont_mul<C28, G>(a, LdsElem{BASE, E}, m28, minv28, g);

@@ -38,6 +38,11 @@ namespace s28 {
 #ifndef EFL_SQR_FIPS
 #define EFL_SQR_FIPS 1
 #endif
+// One-lane multiplies by a register operand by product scanning (mul_fips1) in the fixed-base walks
+// (build knob for A/B: EFL_MUL_FIPS=0 builds the CIOS loop through LDS)
+#ifndef EFL_MUL_FIPS
+#define EFL_MUL_FIPS 1
+#endif
 
 constexpr int kBits = 28;
 constexpr uint32_t kMask = (1u << kBits) - 1;
@@ -167,6 +172,47 @@ __device__ __forceinline__ void sqr_fips1(uint32_t (&a)[C], const uint32_t (&m)[
     carry = t >> kBits;
   }
   a[C - 1] = (uint32_t)carry;          // < 2^28: the result is < 2m < R
+}
+
+// a <- a b R^-1 mod m for numbers held in ONE lane, b in registers too (the fixed-base walk's table
+// entry, loaded straight from HBM): product scanning as in sqr_fips1, without the symmetry. Column k
+// takes a_i b_(k-i) and the reduction's u_i m_(k-i); 2 C^2 limb products like CIOS, but CIOS in one
+// lane runs its steps as a loop whose 64-bit accumulator array shifts down one position per step (2 C
+// register moves per 2 C products) and reads b_i from LDS; here the columns are unrolled, nothing
+// moves, and nothing goes through LDS. Four accumulators per column (two chains of a b, two of
+// m u) keep the dependent mads apart. Bounds as sqr_fips1: a column holds at most C products a b,
+// C products m u and a carry < 2^36: < (2C + 1) 2^56 < 2^64 for C < 127; output < 2m for inputs
+// < 2m (R > 4m). a_(k-C) is written once column k no longer reads it.
+template <int C>
+__device__ __forceinline__ void mul_fips1(uint32_t (&a)[C], const uint32_t (&b)[C], const uint32_t (&m)[C],
+                                          uint32_t minv) {
+  static_assert(C < 127, "column accumulator bound");
+  uint32_t u[C];
+  uint64_t carry = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * C - 1; ++k) {
+    const int ilo = k < C ? 0 : k - C + 1;
+    uint64_t x0 = carry, x1 = 0, r0 = 0, r1 = 0;
+#pragma unroll
+    for (int i = ilo; i <= k && i < C; ++i) {      // a_i b_(k-i), k - i in [0, C)
+      if ((i & 1) == 0) x0 = (uint64_t)a[i] * b[k - i] + x0;
+      else x1 = (uint64_t)a[i] * b[k - i] + x1;
+    }
+#pragma unroll
+    for (int i = ilo; i < k && i < C; ++i) {       // u_i m_(k-i), k - i in [1, C)
+      if ((i & 1) == 0) r0 = (uint64_t)m[k - i] * u[i] + r0;
+      else r1 = (uint64_t)m[k - i] * u[i] + r1;
+    }
+    uint64_t t = x0 + x1 + r0 + r1;
+    if (k < C) {
+      u[k] = ((uint32_t)t * minv) & kMask;
+      t = (uint64_t)m[0] * u[k] + t;   // now 0 mod 2^28
+    } else {
+      a[k - C] = (uint32_t)t & kMask;
+    }
+    carry = t >> kBits;
+  }
+  a[C - 1] = (uint32_t)carry;
 }
 
 // a <- a^2 R^-1 mod m through the element's LDS scratch array (limb i at scratch[i * E]); one-lane

@@ -44,6 +44,19 @@ run() {
             timeout -k 10 600 python -u tools/table_window_probe.py --crt --n-bytes 512 --a-bytes 256 --group 1 --sizes 65536 12 14 15 \
               > gpurun_out/r04_table_window_4096.jsonl 2> gpurun_out/r04_table_window_4096.err ;;
     decfam) timeout -k 10 600 python -u tools/sweep_dec_family.py > gpurun_out/r04_dec_family.jsonl 2> gpurun_out/r04_dec_family.err ;;
+    fipst)  timeout -k 10 900 python -u -m pytest tests/test_paillier_gpu.py tests/test_paillier_crt_gpu.py \
+              tests/test_paillier_key_sizes_gpu.py tests/test_paillier_scalar_gpu.py -m gpu -x -q --timeout 300 \
+              --timeout-method thread > gpurun_out/r04_fips_tests.log 2>&1 ;;
+    fipsab) for nb in 128; do
+              for lib in ${AB_LIBS:-libefl_hip.so libefl_hip_nofips.so}; do
+                WP_NBYTES=$nb EFL_HIP_LIB=$LIBDIR/$lib timeout -k 10 300 python -u tools/walk_probe.py \
+                  >> gpurun_out/r04_fips_walk.jsonl 2>> gpurun_out/r04_fips_walk.err || exit 1
+              done
+            done
+            for lib in ${AB_LIBS:-libefl_hip.so libefl_hip_nofips.so}; do
+              EFL_HIP_LIB=$LIBDIR/$lib timeout -k 10 600 python -u bench.py --stage p --no-cpu-baseline \
+                >> gpurun_out/r04_fips_stagep.jsonl 2>> gpurun_out/r04_fips_stagep.err || exit 1
+            done ;;
     *) echo "unknown step $1"; return 2 ;;
   esac
 }
