@@ -1062,11 +1062,11 @@ class PaillierKeypair(object):
         minimum over j, and the terms of an output multiplied mod n^2. Used when the exponents spread
         past MATMUL_MAX_SPREAD: the shifts then run through _exp2_chunked's bounded launches. The
         product is exact, so the ciphertexts equal efl_pl_matmul's; rows go in chunks of about
-        256 MiB of terms."""
+        _COMPOSED_CHUNK_BYTES (256 MiB) of terms."""
         k = self.key
         u, v = x.shape
         w = ym.shape[1]
-        rows = max(1, (256 << 20) // (v * w * k.lc * 4))
+        rows = max(1, _COMPOSED_CHUNK_BYTES // (v * w * k.lc * 4))
         zs, ms = [], []
         for i0 in range(0, u, rows):
             i1 = min(u, i0 + rows)
@@ -1173,6 +1173,7 @@ _SHIFT_CHUNK = MAX_SHIFT   # squarings per launch of _exp2_chunked (tests lower 
 # runs as the reference's per-term composition (_matmul_composed) instead of one efl_pl_matmul,
 # whose bit-level loop would spend that many squarings per output in one launch
 MATMUL_MAX_SPREAD = MAX_SHIFT
+_COMPOSED_CHUNK_BYTES = 256 << 20   # terms of _matmul_composed per row chunk
 
 
 

@@ -86,8 +86,8 @@ def _matmul_inputs(kp, seed, u=3, v=5, w=4):
 @pytest.mark.parametrize("k,c", fams(ALL))
 def test_matmul_composed_equals_the_kernel(efl, pc, monkeypatch, k, c):
     """The term-by-term matmul (forced with MATMUL_MAX_SPREAD = 0) gives efl_pl_matmul's ciphertexts
-    and exponents bit for bit, in every family; an odd inner size exercises the product tree's
-    carried column."""
+    and exponents bit for bit, in every family, in one row chunk and one row per chunk; an odd
+    inner size exercises the product tree's carried column."""
     kp = keypair(efl, k)
     ct, xe, ym, ye = _matmul_inputs(kp, 31, v=5)
     args = (ct.tensor, torch.from_numpy(xe), torch.from_numpy(ym), torch.from_numpy(ye))
@@ -95,13 +95,15 @@ def test_matmul_composed_equals_the_kernel(efl, pc, monkeypatch, k, c):
         zk, ek = kp.matmul(*args)
         monkeypatch.setattr(pc, "MATMUL_MAX_SPREAD", 0)
         zc, ec = kp.matmul(*args)
-    assert torch.equal(ek.cpu(), ec.cpu())
-    assert zk.to_hex().to_ints() == zc.to_hex().to_ints()
+        monkeypatch.setattr(pc, "_COMPOSED_CHUNK_BYTES", 1)     # one row per chunk
+        zr, er = kp.matmul(*args)
+    assert torch.equal(ek.cpu(), ec.cpu()) and torch.equal(ek.cpu(), er.cpu())
+    assert zk.to_hex().to_ints() == zc.to_hex().to_ints() == zr.to_hex().to_ints()
 
 
 def test_matmul_wide_exponent_spread(efl, pc):
     """Exponents spread by 70,000 (past one launch's squarings): the composed path against the
-    oracle, and the decrypted plaintexts carry sum_j xm*ym*2^(xe+ye-min)."""
+    oracle, ciphertexts and exponents."""
     k = ENC_KEYS[0]
     kp, okp = keypair(efl, k), okeypair(k)
     ct, xe, ym, ye = _matmul_inputs(kp, 32, u=2, v=3, w=2)
