@@ -23,6 +23,8 @@ KEYS = ((64, 32, 1, 262144, (0, 8, 16, 32)), (128, 64, 10, 262144, (0, 8, 16, 32
         (256, 128, 1, 131072, (0, 8, 16, 32)), (512, 256, 1, 65536, (8, 16, 32)))
 if os.environ.get("PLFAM_KEYS"):
     KEYS = tuple(k for k in KEYS if str(8 * k[0]) in os.environ["PLFAM_KEYS"].split(","))
+if os.environ.get("PLFAM_N"):          # e.g. 100352: the MNIST activation's element count
+    KEYS = tuple(k[:3] + (int(os.environ["PLFAM_N"]),) + k[4:] for k in KEYS)
 for n_bytes, a_bytes, g, N, fams in KEYS:
     n, hs, p, q = pc.generate_keypair_ints(n_bytes, 24, random.Random(n_bytes))
     ln = n_bytes // 4
