@@ -247,8 +247,10 @@ int efl_pl_powm(const void* key_block, const efl_pl_key* key, const uint32_t* x,
 
 /* PaillierMulExp2<int64> (paillier.cc:680-751; the int32 variant after widening): z = x^(2^y) mod
  * n^2, y squarings per element, no host-side exponent. y < 0 is the op's InvalidArgument "y should
- * be a positive tensor." (:724-726, :740-742); so is y > 65536 here (the reference
- * would spend hours there). bad (device, one int64) <- -1, or the smallest such index (its z is 0). */
+ * be a positive tensor." (:724-726, :740-742). One launch squares at most 65536 times per element:
+ * y > 65536 is reported like y < 0, and the caller cuts such shifts into launches of at most 65536
+ * squarings, x^(2^(a+b)) = (x^(2^a))^(2^b) (efl.privacy.paillier_cipher _exp2_chunked).
+ * bad (device, one int64) <- -1, or the smallest such index (its z is 0). */
 int efl_pl_mul_exp2(const void* key_block, const efl_pl_key* key, const uint32_t* x, const int64_t* y,
                     uint32_t* z, int64_t n, int64_t* bad, void* stream);
 
@@ -270,7 +272,8 @@ int efl_pl_mul_scalar_big(const void* key_block, const efl_pl_key* key, const ui
 /* FixedPointTensor.__add__ with encrypted mantissas (python/efl/privacy/paillier.py:116-133):
  * z = x^(2^(xe - m)) * y^(2^(ye - m)) mod n^2, m = min(xe, ye) (the caller keeps m as the exponent):
  * the reference's (x << dl) + (y << dr), i.e. two PaillierMulExp2 and one PaillierAdd, fused into
- * one launch. |xe - ye| > 65536 -> bad as in efl_pl_mul_exp2. */
+ * one launch. |xe - ye| > 65536 -> bad as in efl_pl_mul_exp2; the caller then runs the reference's
+ * composition with chunked shifts. */
 int efl_pl_fxp_add(const void* key_block, const efl_pl_key* key, const uint32_t* x, const int64_t* x_exponent,
                    const uint32_t* y, const int64_t* y_exponent, uint32_t* z, int64_t n, int64_t* bad,
                    void* stream);
@@ -288,7 +291,10 @@ int efl_pl_invert(const void* key_block, const efl_pl_key* key, const uint32_t* 
  * kernels first write x R mod n^2 and its odd powers for every x (u*v*16 padded radix-2^28
  * numbers), then every output's multiply schedule (u*w*S lists of up to 5*ceil(v/S) 32-bit words,
  * S the term split) into scratch taken and released on `stream` (hipMallocAsync / hipFreeAsync);
- * a failed allocation returns the HIP error. */
+ * a failed allocation returns the HIP error. An output squares its accumulator once per bit level,
+ * up to the exponent spread (max - min of xe + ye over its terms) plus the top bit of |y|: the
+ * Python host runs a product whose spread may pass 65536 term by term instead (PaillierMulScalar,
+ * chunked PaillierMulExp2, PaillierAdd), so no launch loops that long. */
 int efl_pl_matmul(const void* key_block, const efl_pl_key* key, const uint32_t* x_mantissa,
                   const int64_t* x_exponent, const int64_t* y_mantissa, const int64_t* y_exponent,
                   uint32_t* z_pos, uint32_t* z_neg, int64_t* z_exponent, int u, int v, int w,
