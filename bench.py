@@ -401,7 +401,7 @@ def stage_p(args):
                          "MiB": round(k.block.numel() * 4 / 2**20, 1)},
                "unit": "elements/s", "higher_is_better": True, "dtype": "u32 limbs",
                "data": "synthetic int64 mantissas in [-2^40, 2^40), deterministic key", **res,
-               "cpu_baseline": None}
+               "library": efl.lib.version(), "cpu_baseline": None}
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = stage_p_cpu(n_bytes, a_bytes, g, p, q, hs, args.cpu_threads, cpu_keys)
             for name in ("encrypt", "decrypt"):

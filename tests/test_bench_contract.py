@@ -64,3 +64,24 @@ def test_pmc_traffic_names_the_shipping_library():
                                  "src-hash"], text=True).strip()
     assert tr["library"].endswith("src " + h), (tr["library"], h)
     assert tr["elements"] == 65536 * 1024
+
+
+def _src_hash():
+    import subprocess
+    return subprocess.check_output(["make", "-s", "-C", os.path.join(ROOT, "elastic-federated-learning-solution_amd"),
+                                    "src-hash"], text=True).strip()
+
+
+def test_records_come_from_the_shipping_library():
+    """The round's BENCH line and Stage P report were measured with the library this tree builds,
+    and the Stage P report carries the GMP CPU baseline of the same run (bench hygiene)."""
+    h = _src_hash()
+    assert _line()["library"].endswith("src " + h)
+    with open(os.path.join(ROOT, "profiles", "r04", "bench_stage_p.jsonl")) as f:
+        lines = [json.loads(ln) for ln in f if ln.startswith("{")]
+    assert len(lines) == 3
+    for d in lines:
+        assert d["library"].endswith("src " + h), d["library"]
+        cb = d["cpu_baseline"]
+        assert cb and cb["kind"] in ("port", "reference") and cb["encrypt"] > 0 and cb["decrypt"] > 0
+        assert d["encrypt"]["vs_cpu"] > 1 and d["decrypt"]["vs_cpu"] > 1
