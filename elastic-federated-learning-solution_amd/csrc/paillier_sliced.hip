@@ -224,15 +224,30 @@ __global__ __launch_bounds__(kSlBlock) SL_OCC void k_fbpowm(Key k, const uint32_
   store_slice<C>(out + i * L, g, acc);
 }
 
-// hs^(a') mod n^2 through the radix-2^28 table (same lookup order as fbpowm_mont), result in
-// NORMAL form as this lane's C 32-bit words. Scratch: B (entry / conversion, L28 words per element).
 // Waves per SIMD the one-lane (G = 1) walk kernels are compiled for (build knob for A/B): with the
 // entry and the product-scanning multiply in registers (s28::mul_fips1) the walk takes about 200
 // VGPRs at 2 waves
 #ifndef EFL_WALK1_WAVES
 #define EFL_WALK1_WAVES 2
 #endif
+// One-lane walks load the next non-zero window's entry while the current product runs (build knob
+// for A/B: 0 loads each entry right before its product)
+#ifndef EFL_WALK1_PREFETCH
+#define EFL_WALK1_PREFETCH 1
+#endif
 
+// entry of table row `row`, column idx (1-based) for this lane's slice
+template <int C28, int L28>
+__device__ __forceinline__ const uint32_t* walk_entry(const uint32_t* table, int row, uint32_t idx, int cols, int g) {
+#if EFL_WALK_PROBE   // latency probe build (tools/walk_probe.py): every product reads entry (0, 0), L2-resident
+  return table + g * C28;
+#else
+  return table + ((int64_t)row * cols + (idx - 1)) * L28 + g * C28;
+#endif
+}
+
+// hs^(a') mod n^2 through the radix-2^28 table (same lookup order as fbpowm_mont), result in
+// NORMAL form as this lane's C 32-bit words. Scratch: B (entry / conversion, L28 words per element).
 template <int C, int G>
 __device__ __forceinline__ void fbpowm28_walk(uint32_t (&acc)[s28::limbs_per_lane(C * G, G)], const Key& k,
                                               uint32_t* A, uint32_t* B, int E, int words,
@@ -244,14 +259,45 @@ __device__ __forceinline__ void fbpowm28_walk(uint32_t (&acc)[s28::limbs_per_lan
   const uint32_t minv28 = k.d.n2_minv28;
   const uint32_t* table = k.at(k.d.off_table28);
   const int cols = k.d.table_cols;
+  if constexpr (G == 1 && EFL_MUL_FIPS && EFL_WALK1_PREFETCH) {
+    // one lane holds the whole number (round 4): entries go straight into registers, and the next
+    // non-zero window's entry is in flight while the current product runs
+    int s = 0, row = 0;
+    auto next_entry = [&]() -> const uint32_t* {
+      for (; s < size; s += W, ++row) {
+        const uint32_t idx = col_bits(A, E, s, size - s < W ? size - s : W, words);
+        if (idx) {
+          const uint32_t* e = walk_entry<C28, L28>(table, row, idx, cols, g);
+          s += W;
+          ++row;
+          return e;
+        }
+      }
+      return nullptr;
+    };
+    const uint32_t* cur = next_entry();
+    uint32_t b[C28], nb[C28];
+    if (cur) {
+#pragma unroll
+      for (int j = 0; j < C28; ++j) b[j] = cur[j];
+    }
+    while (cur) {
+      const uint32_t* nxt = next_entry();
+      if (nxt) {
+#pragma unroll
+        for (int j = 0; j < C28; ++j) nb[j] = nxt[j];
+      }
+      s28::mul_fips1<C28>(acc, b, m28, minv28);
+      cur = nxt;
+#pragma unroll
+      for (int j = 0; j < C28; ++j) b[j] = nb[j];
+    }
+    return;
+  }
   for (int s = 0, row = 0; s < size; s += W, ++row) {
     const uint32_t idx = col_bits(A, E, s, size - s < W ? size - s : W, words);
     if (idx) {
-#if EFL_WALK_PROBE   // latency probe build (tools/walk_probe.py): every product reads entry (0, 0), L2-resident
-      const uint32_t* ent = table + g * C28;
-#else
-      const uint32_t* ent = table + ((int64_t)row * cols + (idx - 1)) * L28 + g * C28;
-#endif
+      const uint32_t* ent = walk_entry<C28, L28>(table, row, idx, cols, g);
       if constexpr (G == 1 && EFL_MUL_FIPS) {
         // one lane holds the whole number: the entry goes straight into registers (round 4)
         uint32_t b[C28];
