@@ -39,6 +39,9 @@ run() {
                 2>> gpurun_out/r04_walk_probe.err || return $?
             done ;;
     rekey)  timeout -k 10 300 python -u tools/rekey_probe.py > gpurun_out/r04_rekey.jsonl 2> gpurun_out/r04_rekey.err ;;
+    keysize) timeout -k 10 300 python -u tools/keysize_probe.py > gpurun_out/r04_keysize.jsonl 2> gpurun_out/r04_keysize.err ;;
+    keytests) timeout -k 10 900 python -u -m pytest tests/test_paillier_key_sizes_gpu.py tests/test_paillier_long_shift_gpu.py \
+              -m gpu -x -q --timeout 600 --timeout-method thread > gpurun_out/r04_keysizes.log 2>&1 ;;
     tblw)   timeout -k 10 600 python -u tools/table_window_probe.py --crt 16 18 20 \
               > gpurun_out/r04_table_window_1024.jsonl 2> gpurun_out/r04_table_window_1024.err && \
             timeout -k 10 600 python -u tools/table_window_probe.py --crt --n-bytes 512 --a-bytes 256 --group 1 --sizes 65536 12 14 15 \
