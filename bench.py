@@ -398,7 +398,7 @@ def stage_p(args):
                                         "group_size": g, "table_window": W, "elements": N},
                "key_setup_ms": round(t_key * 1e3, 1), "public_table_setup_ms": round(t_tab * 1e3, 1),
                "table": {"rows": k.desc.table_rows, "cols": k.desc.table_cols,
-                         "MiB": round(k.block.numel() * 4 / 2**20, 1)},
+                         "MiB": round(k.block_bytes / 2**20, 1)},
                "unit": "elements/s", "higher_is_better": True, "dtype": "u32 limbs",
                "data": "synthetic int64 mantissas in [-2^40, 2^40), deterministic key", **res,
                "library": efl.lib.version(), "cpu_baseline": None}
@@ -432,7 +432,7 @@ def stage_p_crt(k, subs, a_bytes, N, t, t_public, t_setup):
                          "frac": round(per_s * macs / MAD_U64_U32_PEAK, 4),
                          "issue_frac_walks": round(per_s * issued / MAD_U64_U32_PEAK, 4)},
             "sub_key_setup_ms": round(t_setup * 1e3, 1),
-            "sub_tables_MiB": round(sum(sk.block.numel() for sk in subs) * 4 / 2**20, 1),
+            "sub_tables_MiB": round(sum(sk.block_bytes for sk in subs) / 2**20, 1),
             "kernel_family": pc_family(subs[0].ln)}
 
 
@@ -759,6 +759,8 @@ def main(argv=None):
 
     ms_per_step = elapsed / args.steps * 1e3
     value = world * (n * 4) / GIB / (elapsed / args.steps)
+    # every rank reports the device it really ran on (PCI location), gathered after the timed region
+    rank_devices = edist.gather_rank_devices(edist.rank_device_info(rank, dev))
 
     # practical peak: device-to-device copy of the same byte volume as one kernel
     copy_gbs = None
@@ -821,8 +823,9 @@ def main(argv=None):
         "d2d_copy_GBs": round(copy_gbs, 1) if copy_gbs else None,
         "seed_broadcast_us": round(bcast_us, 2),
         "backend": backend if world > 1 else None,
-        "devices_used": 1 if world == 1 else min(world, torch.cuda.device_count()),
+        "devices_used": edist.distinct_devices(rank_devices),
         "devices_visible": torch.cuda.device_count(),
+        "rank_devices": rank_devices,
         "library": efl.lib.version(),
         "cpu_baseline": None,
     }

@@ -78,6 +78,51 @@ def all_reduce_max(values, group=None):
     return t.tolist()
 
 
+def rank_device_info(rank: int, dev=None) -> dict:
+    """What this rank really runs on, observed rather than inferred: host name, the current HIP
+    device index and its PCI location (domain:bus:device) and UUID from the device properties.
+    dev None (a CPU rank): device fields are None."""
+    import socket
+    info = {"rank": int(rank), "host": socket.gethostname(), "device": None, "pci": None, "uuid": None,
+            "name": None}
+    if dev is None:
+        return info
+    idx = torch.device(dev).index
+    idx = torch.cuda.current_device() if idx is None else idx
+    prop = torch.cuda.get_device_properties(idx)
+    info["device"] = int(idx)
+    info["name"] = prop.name
+    bus = getattr(prop, "pci_bus_id", None)
+    if bus is not None:
+        info["pci"] = "%04x:%02x:%02x" % (int(getattr(prop, "pci_domain_id", 0)), int(bus),
+                                          int(getattr(prop, "pci_device_id", 0)))
+    u = getattr(prop, "uuid", None)
+    info["uuid"] = str(u) if u is not None else None
+    return info
+
+
+def gather_rank_devices(info: dict, group=None) -> list:
+    """Every rank's rank_device_info, in rank order, on every rank (all_gather_object; a single
+    process returns [info])."""
+    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return [info]
+    out = [None] * dist.get_world_size(group)
+    dist.all_gather_object(out, info, group=group)
+    return sorted(out, key=lambda d: d["rank"])
+
+
+def distinct_devices(rank_devices) -> int:
+    """Number of distinct GPUs the ranks ran on: (host, PCI location) when the PCI location is
+    known, else (host, UUID), else (host, device index). CPU ranks count none."""
+    keys = set()
+    for d in rank_devices:
+        if d.get("device") is None:
+            continue
+        ident = d.get("pci") or d.get("uuid") or ("index", d["device"])
+        keys.add((d.get("host"), ident))
+    return len(keys)
+
+
 def broadcast_key_material(seed: bytes | None = None, public_key: dict | None = None, src: int = 0,
                            group=None):
     """Broadcast {seed (32 B), public key} from `src`; returns (seed, public_key) on every rank.

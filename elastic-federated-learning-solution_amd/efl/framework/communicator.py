@@ -416,8 +416,13 @@ class Communicator(object):
             self._inflight[name] = fut
 
         def forget(_):
-            if self._inflight.get(name) is fut:
-                self._inflight.pop(name, None)
+            # compare-and-pop under the lock: a send of the same name may store its successor
+            # between the check and the pop, and popping that successor would let a third send
+            # run beside it. Never re-entered with the lock held: forget is attached only here,
+            # after the `with` block, and nothing completes `fut` under the lock afterwards.
+            with self._lock:
+                if self._inflight.get(name) is fut:
+                    del self._inflight[name]
         fut.add_done_callback(forget)
         return fut
 

@@ -19,6 +19,7 @@ import hashlib
 import math
 import os
 import secrets
+import weakref
 
 import numpy as np
 import torch
@@ -105,42 +106,23 @@ SLICINGS = {16: ([0, 8, 16, 32], [0, 8]), 32: ([0, 8, 16, 32], [0, 8, 16, 32]), 
             128: ([8, 16, 32], [0, 8, 16, 32]), 256: ([32], [8, 16, 32])}
 
 _LIMB_CLASSES = (16, 32, 64, 128, 256)
-MAX_TABLE_BITS = 1 << 40      # gmp_utils.h:20 FBPOWM_MAX_TABLE_MEM, compared against entries x bits
-# above this the radix-2^28 copy of the fixed-base table is not built (a table chosen under
-# TABLE_MAX_BYTES always has it; an explicit table_window up to 24 may ask for more)
-TABLE28_MAX_BYTES = 1 << 36
 
-
-def _limbs28_rows(vals, L: int, nbytes: int) -> np.ndarray:
-    """Many ints -> [len(vals), L] radix-2^28 limbs (vectorised through the little-endian bits)."""
-    raw = np.frombuffer(b"".join(v.to_bytes(nbytes, "little") for v in vals), dtype=np.uint8)
-    bits = np.unpackbits(raw.reshape(len(vals), nbytes), axis=1, bitorder="little")
-    need = 28 * L
-    if bits.shape[1] < need:
-        bits = np.pad(bits, ((0, 0), (0, need - bits.shape[1])))
-    w = (1 << np.arange(28, dtype=np.uint32)).astype(np.uint32)
-    return (bits[:, :need].reshape(len(vals), L, 28).astype(np.uint32) * w).sum(axis=2, dtype=np.uint32)
-
-
-# Device memory the fixed-base table of one key may take, both layouts (round 3; round 2 capped the
-# table at 2^18 entries whatever their size). A fresh-randomness encryption costs
-# ceil(a_bits / W) (1 - 2^-W) table products, so the widest window that fits is the fastest; the
-# lookups of a table larger than the 256 MB Infinity Cache are random HBM reads, and they still pay
-# (tools/table_window_probe.py, profiles/r03/table_window_*.jsonl): the examples' 1024-bit key
-# 53.9 -> 69.6 M encrypts/s from W = 12 to 16 (1.1 GiB table), the reference default 4096-bit key
-# 823 k -> 979 k/s from W = 10 to 12 (1.4 GiB). 1.5 GiB is about half a percent of a 288 GB HBM.
-# Round 4: 4 GiB per keypair (profiles/r04/table_window_*.jsonl: the 1024-bit key 65.2 -> 76.2 M
-# encrypts/s from W = 16 to 18 (4.0 GiB), 80.8 M/s at W = 20 (14 GiB); the 4096-bit key 0.99 -> 1.07
-# -> 1.14 -> 1.22 -> 1.31 M/s from W = 12 to 16 (1.4 -> 17.7 GiB)). A public-key holder spends it on
-# its one table; the key owner, whose encryptions go by CRT, on the two CRT sub-tables (half each),
-# building its n^2 table only if it is ever walked (KeyBlock.ensure_table). About 1.4 % of a 288 GB
-# HBM; EFL_PL_TABLE_MAX_MIB overrides it.
+# Device memory the fixed-base tables may take (csrc/keyset.hip sizes them; round 3 measured why the
+# widest window that fits is the fastest: a fresh-randomness encryption costs ceil(a_bits / W)
+# (1 - 2^-W) table products, and lookups past the 256 MB Infinity Cache still pay:
+# profiles/r03/table_window_*.jsonl, profiles/r04/table_window_*.jsonl: the 1024-bit key 65.2 -> 76.2
+# M encrypts/s from W = 16 to 18 (4.0 GiB), the 4096-bit key 0.99 -> 1.07 M/s from W = 12 to 13).
+# Two bounds (round 5): a cap per keypair, TABLE_MAX_BYTES (EFL_PL_TABLE_MAX_MIB), and one
+# PROCESS-WIDE budget shared by every live keypair (table_budget(); EFL_PL_TABLE_BUDGET_MIB, default
+# 4 GiB): a key's window is the widest whose table fits the smaller of its cap and what the budget has
+# left. A public-key holder spends it on its one table; the key owner, whose encryptions go by CRT, on
+# the two CRT sub-tables (3/8 each), building its n^2 table from the rest only if it is ever walked.
 TABLE_MAX_BYTES = 4 << 30
 WINDOW_MAX = 24
 
 
 def table_max_bytes() -> int:
-    """The per-keypair table budget: EFL_PL_TABLE_MAX_MIB (MiB) if set, else TABLE_MAX_BYTES."""
+    """The per-keypair table cap: EFL_PL_TABLE_MAX_MIB (MiB) if set, else TABLE_MAX_BYTES."""
     v = os.environ.get("EFL_PL_TABLE_MAX_MIB", "")
     return int(v) << 20 if v else TABLE_MAX_BYTES
 
@@ -148,33 +130,20 @@ def table_max_bytes() -> int:
 def choose_table_window(a_bits: int, entry_bytes: int, max_bytes: int | None = None) -> int:
     """Widest window W <= WINDOW_MAX whose table (ceil(a_bits / W) rows x 2^W - 1 entries of
     entry_bytes: the n^2 words of every layout the key keeps) fits max_bytes (default
-    table_max_bytes()). With 4 GiB: 2048-bit a of a 4096-bit n (the reference default) -> W = 13,
-    512-bit a of a 1024-bit n (the examples) -> W = 18."""
+    table_max_bytes()); the library's own rule (efl_pl_choose_window), 1 when none fits. With 4 GiB:
+    2048-bit a of a 4096-bit n (the reference default) -> W = 13, 512-bit a of a 1024-bit n (the
+    examples) -> W = 18."""
     if max_bytes is None:
         max_bytes = table_max_bytes()
-    best = 1
-    for W in range(1, WINDOW_MAX + 1):
-        if -(-a_bits // W) * ((1 << W) - 1) * entry_bytes > max_bytes:
-            break
-        best = W
-    return best
+    return max(1, _lib.efl_pl_choose_window(int(a_bits), int(entry_bytes), int(max_bytes)))
 
 
 def _limbs(x: int, L: int) -> np.ndarray:
     return np.frombuffer(int(x).to_bytes(4 * L, "little"), dtype="<u4").copy()
 
 
-def _minv32(m: int) -> int:
-    return (-pow(m, -1, 1 << 32)) % (1 << 32)
-
-
-def _limbs28(x: int, L: int) -> np.ndarray:
-    """x as L radix-2^28 limbs, one per 32-bit word (csrc/sliced28.h)."""
-    return np.array([(x >> (28 * k)) & 0xFFFFFFF for k in range(L)], dtype="<u4")
-
-
 def table_passes(W: int, cols: int):
-    """The table build's doubling passes (KeyBlock._build_table): pass k computes the columns
+    """The table build's doubling passes (csrc/keyset.hip build_table): pass k computes the columns
     (0-based) lo .. lo + cnt - 1, lo = 2^k, as column i times b^(2^k) for i in 0 .. cnt - 1, so column
     c holds b^(c + 1) and every source column was made by an earlier pass."""
     out = []
@@ -315,6 +284,10 @@ def generate_keypair_ints(n_bytes=512, reps=24, rng=None, batch=None):
     get their `reps` Miller-Rabin rounds on host threads in native code (efl_host_probable_primes);
     the first probable prime in draw order is taken. hs is computed by CRT mod p^2 and q^2
     (efl_host_powm) and joined: the same value as the reference's mpz_powm mod n^2."""
+    if n_bytes < 16:
+        # the device kernels need n of at least 128 bits (KeyBlock refuses smaller keys), and the
+        # sieve below discards every prime of 16 bits or fewer: refuse before the prime search
+        raise errors.UnimplementedError("n of fewer than 128 bits is not supported on the GPU")
     rng = rng or secrets.SystemRandom()
     bits = n_bytes * 4
     if batch is None:
@@ -352,296 +325,243 @@ def hs_of(x: int, p: int, q: int) -> int:
 # device key block
 # ----------------------------------------------------------------------------------------------
 
+class PlCtxInfo(ctypes.Structure):
+    """ctypes mirror of efl_pl_ctx_info (include/efl_hip.h)."""
+    _fields_ = [(n, ctypes.c_int32) for n in ("has_public", "has_private", "n_bytes", "ln", "a_bits", "group_size",
+                                               "table_window", "has_table", "crt_capable", "crt")] + \
+               [("crt_table_window", ctypes.c_int32 * 2)] + \
+               [(n, ctypes.c_int64) for n in ("block_bytes", "table_bytes", "table_max_bytes")] + \
+               [("crt_block_bytes", ctypes.c_int64 * 2), ("crt_table_bytes", ctypes.c_int64 * 2),
+                ("generation", ctypes.c_uint64)]
+
+
+_cp = ctypes.c_char_p
+for _name, _args, _res in (
+        ("efl_pl_ctx_create", [ctypes.POINTER(_vp)], _i32),
+        ("efl_pl_ctx_destroy", [_vp], _i32),
+        ("efl_pl_ctx_options", [_vp, _i64, _i32, _i32], _i32),
+        ("efl_pl_set_public", [_vp, _cp, _i32, _cp, _i32, _i32, _vp], _i32),
+        ("efl_pl_set_private", [_vp, _cp, _cp, _vp], _i32),
+        ("efl_pl_set_keypair", [_vp, _cp, _i32, _cp, _i32, _i32, _cp, _cp, _vp], _i32),
+        ("efl_pl_ctx_key", [_vp, _i32, ctypes.POINTER(_vp), _PK], _i32),
+        ("efl_pl_ctx_prepare", [_vp, _i32, _vp], _i32),
+        ("efl_pl_ctx_query", [_vp, ctypes.POINTER(PlCtxInfo)], _i32),
+        ("efl_pl_ctx_copy", [_vp, _i32, _i64, _i64, _vp, _vp], _i32),
+        ("efl_pl_ctx_encrypt", [_vp, _vp, _vp, _vp, _i64, _u64, _i64, _i32, _vp], _i32),
+        ("efl_pl_ctx_fbpowm", [_vp, _vp, _vp, _i64, _u64, _i64, _i32, _vp], _i32),
+        ("efl_pl_ctx_decrypt", [_vp, _vp, _vp, _vp, _i64, _vp], _i32),
+        ("efl_pl_table_budget", [_i64, ctypes.POINTER(_i64)], _i64),
+        ("efl_pl_choose_window", [_i32, _i64, _i64], _i32),
+        ("efl_pl_key_derive", [_cp, _cp, _i32, _i32, _cp, _cp, _cp, _i32, _i64, _vp, ctypes.POINTER(_i64), _PK],
+         _i32)):
+    getattr(_lib, _name).argtypes = _args
+    getattr(_lib, _name).restype = _res
+
+PREPARE_TABLE, PREPARE_CRT, PUBLIC_PATH = 1, 2, 1
+
+
+def _hx(x: int) -> bytes:
+    return format(int(x), "x").encode()
+
+
+def table_budget(nbytes: int | None = None):
+    """The process-wide device-memory budget of the fixed-base tables (efl_pl_table_budget):
+    returns (budget, bytes in use) after setting it to `nbytes` if given."""
+    used = _i64(0)
+    prev = _lib.efl_pl_table_budget(-1 if nbytes is None else int(nbytes), ctypes.byref(used))
+    cur = prev if nbytes is None else int(nbytes)
+    return cur, used.value
+
+
+class _KeyView:
+    """One key block of a context (which 0 = the key, 1 / 2 = the CRT sub-keys): what the efl_pl_*
+    ops take, fetched from the library on every use (a key set again moves the block)."""
+
+    def __init__(self, owner: "KeyBlock", which: int, n: int, ln: int):
+        # a weak reference: the key's views must not keep it (and its device memory) alive in a cycle
+        self._ref, self.which, self.n, self.ln = weakref.ref(owner), which, n, ln
+        self.lc, self.lh = 2 * ln, ln // 2
+        self.device = owner.device
+        self._desc = PlKey()
+
+    def args(self):
+        ptr = _vp()
+        _efl_lib.check(_lib.efl_pl_ctx_key(self._owner.ctx, self.which, ctypes.byref(ptr), ctypes.byref(self._desc)))
+        return ptr.value, ctypes.byref(self._desc)
+
+    @property
+    def _owner(self) -> "KeyBlock":
+        o = self._ref()
+        if o is None or not o.ctx:
+            raise errors.AbortedError("the key this view belongs to was released")
+        return o
+
+    @property
+    def desc(self) -> PlKey:
+        self.args()
+        return self._desc
+
+    @property
+    def table_window(self) -> int:
+        return self.desc.table_window
+
+    @property
+    def block_bytes(self) -> int:
+        i = self._owner.info()
+        return i.block_bytes if self.which == 0 else i.crt_block_bytes[self.which - 1]
+
+    def read_words(self, off: int, count: int) -> np.ndarray:
+        """count 32-bit words of this key block from word `off` (efl_pl_ctx_copy), as uint32."""
+        out = np.empty(count, dtype="<u4")
+        with torch.cuda.device(self.device):
+            _efl_lib.check(_lib.efl_pl_ctx_copy(self._owner.ctx, self.which, off, count, out.ctypes.data, None))
+            torch.cuda.synchronize(self.device)
+        return out
+
+
 class KeyBlock:
-    """Host derivation + device upload of every constant the kernels read (efl_pl_key)."""
+    """A Paillier key in device memory: the library's key context (efl_pl_ctx, csrc/keyset.hip),
+    which derives every constant the kernels read from the key's hex text, builds the fixed-base
+    table on the device, and keeps the key owner's CRT sub-keys. This class is the thin Python
+    handle: the reference's PaillierKeypair resource (paillier.cc:50-101) on the host side of the
+    C ABI (include/efl_hip.h, "Key context")."""
 
     def __init__(self, n: int, hs: int, a_bits: int, group_size: int, p=None, q=None, device=None,
-                 table_window=None, reuse_table=None, walk_start=None, max_bytes=None, defer_table=None):
-        """walk_start: the fixed-base walk's accumulator starts from walk_start (mod n^2) instead of 1,
-        so efl_pl_fbpowm gives walk_start * hs^(a') mod n^2 (the CRT keys of crt_keys). max_bytes:
-        the table's byte budget (default table_max_bytes()). defer_table: build the fixed-base table
-        on its first use (ensure_table) instead of now; None = defer exactly when the key owner's
-        encryption goes by CRT (crt_capable), which never walks this table."""
-        if n.bit_length() < 128:
-            raise errors.UnimplementedError("n of fewer than 128 bits is not supported on the GPU")
-        if p is not None and q is not None and p == q:
-            # q^-1 mod p does not exist: the reference's mpz_invert fails silently there and its
-            # decryption is wrong (paillier.cc:88-99); refuse the key instead
-            raise errors.InvalidArgumentError("private key: p and q must be distinct")
-        if p is not None and q is not None and q >= 2 * p:
-            p, q = q, p        # CRT below reduces mq mod p with one subtraction: needs q < 2p
-        self.n, self.hs, self.p, self.q = n, hs, p, q
-        self.a_bits, self.group_size = a_bits, group_size
-        self._window_arg = table_window     # an explicit window also sizes the CRT sub-tables
-        self._max_bytes = table_max_bytes() if max_bytes is None else int(max_bytes)
-        need = max(n.bit_length(), 2 * max(p or 0, q or 0).bit_length())
-        ln = next((c for c in _LIMB_CLASSES if 32 * c >= need), None)
-        if ln is None:
-            raise errors.UnimplementedError(f"n of {n.bit_length()} bits: at most 8192 supported")
-        self.ln, self.lc, self.lh = ln, 2 * ln, ln // 2
-        if a_bits <= 0 or a_bits > 8192:
-            raise errors.InvalidArgumentError("a_bytes must be in [1, 1024]")
-        if group_size < 1 or group_size > 20:
-            raise errors.InvalidArgumentError("group_size must be in [1, 20]")
+                 table_window=None, max_bytes=None, n_bytes=None):
+        """Set (n, hs) and, with p and q, the private key, in one call (efl_pl_set_keypair, or
+        efl_pl_set_public). max_bytes: the context's table cap (default EFL_PL_TABLE_MAX_MIB or 4
+        GiB); the process-wide budget (table_budget) bounds it further. table_window forces the
+        window (1..24; results never depend on it)."""
+        KeyBlock.check(n, hs, a_bits, group_size, p, q, table_window)     # refusals before the device
         self.device = device or _efl_lib.require_gpu()
-        self.desc = PlKey()
-        words = []
-        pos = [0]
+        ctx = _vp()
+        _efl_lib.check(_lib.efl_pl_ctx_create(ctypes.byref(ctx)))
+        self.ctx = ctx.value
+        self._views = {}
+        self._crt_views = None
+        try:
+            _efl_lib.check(_lib.efl_pl_ctx_options(self.ctx, -1 if max_bytes is None else int(max_bytes),
+                                                   int(table_window or 0), -1))
+            self.set(n, hs, a_bits, group_size, p, q, n_bytes)
+        except Exception:
+            self.close()
+            raise
 
-        def put(x: int, L: int) -> int:
-            off = pos[0]
-            words.append(_limbs(x, L))
-            pos[0] += L
-            return off
+    @staticmethod
+    def check(n: int, hs: int, a_bits: int, group_size: int, p=None, q=None, table_window=None):
+        """Everything setting this key could refuse on the host (arguments, sizes, the reference's
+        table guard), without the device (efl_pl_key_derive); raises the error setting it would."""
+        if a_bits % 8:
+            raise errors.InvalidArgumentError("a_bits must be a whole number of bytes")
+        words = _i64(0)
+        d = PlKey()
+        priv = p is not None and q is not None
+        _efl_lib.check(_lib.efl_pl_key_derive(_hx(n), _hx(hs), int(a_bits) // 8, int(group_size),
+                                              _hx(p) if priv else None, _hx(q) if priv else None, None,
+                                              int(table_window or 0), 1 << 62, None, ctypes.byref(words),
+                                              ctypes.byref(d)))
 
-        d = self.desc
-        n2 = n * n
-        Rc = 1 << (32 * self.lc)
-        d.ln, d.a_bits, d.group_size = ln, a_bits, group_size
-        d.off_n = put(n, ln)
-        d.off_n2 = put(n2, self.lc)
-        d.off_n2_r2 = put(Rc * Rc % n2, self.lc)
-        d.off_n2_one = put(Rc % n2, self.lc)
-        d.off_max = put(-(-(2 * n) // 3), ln)
-        d.n2_minv = _minv32(n2)
-        if p is not None and q is not None:
-            Rp, Rh = 1 << (32 * ln), 1 << (32 * self.lh)
-            d.has_private = 1
-            d.off_p, d.off_q = put(p, self.lh), put(q, self.lh)
-            d.off_p2, d.off_q2 = put(p * p, ln), put(q * q, ln)
-            d.p2_minv, d.q2_minv = _minv32(p * p), _minv32(q * q)
-            d.p_minv, d.q_minv = _minv32(p), _minv32(q)
-            d.off_p2_r3 = put(pow(Rp, 3, p * p), ln)
-            d.off_q2_r3 = put(pow(Rp, 3, q * q), ln)
-            d.off_pm1, d.off_qm1 = put(p - 1, self.lh), put(q - 1, self.lh)
-            d.pm1_bits, d.qm1_bits = (p - 1).bit_length(), (q - 1).bit_length()
-            d.off_pinv_w = put(pow(p, -1, Rh), self.lh)
-            d.off_qinv_w = put(pow(q, -1, Rh), self.lh)
-            hp = pow((pow(n + 1, p - 1, p * p) - 1) // p, -1, p)      # paillier.cc:28-37
-            hq = pow((pow(n + 1, q - 1, q * q) - 1) // q, -1, q)
-            d.off_hp = put(hp * Rh % p, self.lh)
-            d.off_hq = put(hq * Rh % q, self.lh)
-            d.off_qinvp = put(pow(q, -1, p) * Rh % p, self.lh)
-            # radix-2^28 constants for the sliced decryption (include/efl_hip.h, csrc/sliced28.h)
-            L28s = [limbs28_total(ln, 1 << k) for k in range(6)]
-            Lmax = max(L28s)
-            d.p2_28_len = Lmax
-
-            def put28(x: int) -> int:
-                off = pos[0]
-                words.append(_limbs28(x, Lmax))
-                pos[0] += Lmax
-                return off
-            d.off_p2_28, d.off_q2_28 = put28(p * p), put28(q * q)
-            d.p2_minv28 = (-pow(p * p, -1, 1 << 28)) % (1 << 28)
-            d.q2_minv28 = (-pow(q * q, -1, 1 << 28)) % (1 << 28)
-            for k, L28 in enumerate(L28s):
-                d.off_p2_r2_28[k] = put28(pow(2, 2 * 28 * L28, p * p))
-                d.off_q2_r2_28[k] = put28(pow(2, 2 * 28 * L28, q * q))
-        # Fixed-base table (gmp_utils.cc:56-89). The reference builds T[i][j] = hs^((j+1) 2^(g i))
-        # with its API group size g and reads it with per-group bit-reversed indices, i.e. it
-        # computes hs^(a'), a' = a with every g-bit group reversed. The kernels form a' themselves
-        # (pl_common.h regroup_exponent) and walk it in plain windows of THIS table's width W,
-        # chosen here for speed: one Montgomery product per non-zero window, so W = 10 cuts the
-        # reference default (4096-bit n, g = 1, 2048-bit a) from ~1024 products per encryption
-        # to ~205. The reference's size guard still applies to the table it would build.
-        g = group_size
-        api_rows = a_bits // g + (1 if a_bits % g else 0)
-        if api_rows * ((1 << g) - 1) * n2.bit_length() > MAX_TABLE_BITS:
-            raise errors.ResourceExhaustedError("Memory usage exceeds a predefined threshold.")
-        # radix-2^28 copy of the table for the sliced family the n^2 kernels use (include/efl_hip.h)
-        fam = kernel_slicing(ln, False)
-        L28 = limbs28_total(2 * ln, 2 * ln // fam) if fam else 0
-        W = int(table_window) if table_window else choose_table_window(a_bits, 4 * (self.lc + L28), self._max_bytes)
-        if not 1 <= W <= 24:
-            raise errors.InvalidArgumentError("table_window must be in [1, 24]")
-        cols = (1 << W) - 1
-        rows = -(-a_bits // W)
-        d.table_rows, d.table_cols, d.table_window = rows, cols, W
-        self.table_window = W
-        d.off_table28 = -1
-        if fam:
-            G = 2 * ln // fam
-            if rows * cols * L28 * 4 <= TABLE28_MAX_BYTES:
-                R28 = 1 << (28 * L28)
-                d.n2_28_len, d.table28_log2g = L28, G.bit_length() - 1
-                d.n2_minv28 = (-pow(n2, -1, 1 << 28)) % (1 << 28)
-                d.off_n2_28 = pos[0]
-                words.append(_limbs28(n2, L28))
-                pos[0] += L28
-                d.off_n2_one28 = pos[0]
-                words.append(_limbs28(R28 % n2, L28))
-                pos[0] += L28
-                d.off_n2_r2_28 = pos[0]
-                words.append(_limbs28(R28 * R28 % n2, L28))
-                pos[0] += L28
+    def set(self, n: int, hs: int, a_bits: int, group_size: int, p=None, q=None, n_bytes=None):
+        """SetPaillierPublicKey (+ SetPaillierPrivateKey) on this context, in place. A refused key
+        (bad argument, unsupported size, the table budget) leaves the previous key in place."""
+        nb = int(n_bytes) if n_bytes is not None else (int(n).bit_length() + 7) // 8
+        with torch.cuda.device(self.device):
+            sh = _stream(self.device)
+            if p is not None and q is not None:
+                rc = _lib.efl_pl_set_keypair(self.ctx, _hx(n), nb, _hx(hs), int(a_bits) // 8, int(group_size),
+                                             _hx(p), _hx(q), sh)
             else:
-                L28 = 0
-        head = torch.from_numpy(np.concatenate(words).view(np.int32)).to(self.device)
-        # the key block without its tables runs the build (n^2 powm / multiply kernels); until a table
-        # is attached the descriptor says so (table_rows 0: the encryption entry points refuse)
-        self._head = head
-        self._tab = (W, rows, cols, L28, d.off_n2_one, walk_start, Rc)
-        d.off_table, d.table_rows, d.off_table28 = -1, 0, -1
-        self.block, self.ptr = head, head.data_ptr()
-        self.has_table = False
-        src = reuse_table
-        if src is not None and getattr(src, "has_table", False) \
-                and (src.n, src.hs, src.a_bits, src.table_window, src.lc) == (n, hs, a_bits, W, self.lc) \
-                and torch.device(src.device) == torch.device(self.device) \
-                and (src.desc.off_table28 >= 0) == bool(L28) and (not L28 or src.desc.n2_28_len == L28):
-            # set_private_key on a key whose public part is unchanged: the tables are the same
-            o32, o28 = src.desc.off_table, src.desc.off_table28
-            self._attach(src.block[o32:o32 + rows * cols * self.lc],
-                         src.block[o28:o28 + rows * cols * L28] if L28 else None)
-        elif not (self.crt_capable() if defer_table is None else defer_table):
-            self.ensure_table()
-        # the key owner's CRT encryption keys (crt_keys), carried over when only the private part
-        # was set again
-        self._crt = None
-        if src is not None and getattr(src, "_crt", None) and (src.p, src.q) == (self.p, self.q) \
-                and (src.hs, src.a_bits, src.group_size) == (hs, a_bits, group_size) \
-                and torch.device(src.device) == torch.device(self.device):
-            self._crt = src._crt
-        torch.cuda.current_stream(self.device).synchronize()
+                rc = _lib.efl_pl_set_public(self.ctx, _hx(n), nb, _hx(hs), int(a_bits) // 8, int(group_size), sh)
+            _efl_lib.check(rc)
+        self._refresh(n, hs, a_bits, group_size, p, q)
 
-    def ensure_table(self):
-        """Build and attach the fixed-base table if this key block has none yet (a deferred table:
-        the key owner's, whose own encryptions go by CRT). Returns self."""
-        if not self.has_table:
-            W, rows, cols, L28, r_one, _, _ = self._tab
-            t32, t28 = self._build_table(self.hs % (self.n * self.n), self.n * self.n, W, rows, cols, self._head,
-                                         r_one, L28)
-            self._attach(t32, t28)
-            torch.cuda.current_stream(self.device).synchronize()
-        return self
+    def set_private(self, p: int, q: int):
+        """SetPaillierPrivateKey in place (the public part and its table stay)."""
+        with torch.cuda.device(self.device):
+            _efl_lib.check(_lib.efl_pl_set_private(self.ctx, _hx(p), _hx(q), _stream(self.device)))
+        self._refresh(self.n, self.hs, self.a_bits, self.group_size, p, q)
 
-    def _attach(self, t32, t28):
-        d = self.desc
-        head = self._head
-        W, rows, cols, L28, _, walk_start, Rc = self._tab
-        n2 = self.n * self.n
-        parts = [head, t32.reshape(-1)]
-        d.table_rows, d.off_table = rows, head.numel()
-        if L28:
-            d.off_table28 = head.numel() + t32.numel()
-            parts.append(t28.reshape(-1))
-        self.block = torch.cat(parts)
-        if walk_start is not None:   # after the table build, which multiplies by the true R mod n^2
-            s0 = walk_start % n2
-            self.block[d.off_n2_one:d.off_n2_one + self.lc] = \
-                torch.from_numpy(_limbs(s0 * Rc % n2, self.lc).view(np.int32)).to(self.device)
-            if L28:
-                self.block[d.off_n2_one28:d.off_n2_one28 + L28] = \
-                    torch.from_numpy(_limbs28(s0 * (1 << (28 * L28)) % n2, L28).view(np.int32)).to(self.device)
-        self.ptr = self.block.data_ptr()
-        self.has_table = True
+    def _refresh(self, n, hs, a_bits, group_size, p, q):
+        self.n, self.hs, self.a_bits, self.group_size = int(n), int(hs), int(a_bits), int(group_size)
+        if p is not None and q is not None:
+            p, q = int(p), int(q)
+            if q >= 2 * p:
+                p, q = q, p              # as the key block orders them (the CRT reduces mq mod p once)
+        self.p, self.q = p, q
+        i = self.info()
+        self.ln, self.lc, self.lh = i.ln, 2 * i.ln, i.ln // 2
+        self._main = _KeyView(self, 0, self.n, self.ln)
+
+    def close(self):
+        ctx, self.ctx = getattr(self, "ctx", None), None
+        if ctx:
+            _lib.efl_pl_ctx_destroy(ctx)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:       # noqa: BLE001 - interpreter shutdown
+            pass
+
+    # -- the key the ops take ------------------------------------------------------------------
+    def args(self):
+        return self._main.args()
+
+    @property
+    def desc(self) -> PlKey:
+        return self._main.desc
+
+    def info(self) -> PlCtxInfo:
+        i = PlCtxInfo()
+        _efl_lib.check(_lib.efl_pl_ctx_query(self.ctx, ctypes.byref(i)))
+        return i
+
+    @property
+    def table_window(self) -> int:
+        return self.info().table_window
+
+    @property
+    def has_table(self) -> bool:
+        return bool(self.info().has_table)
+
+    @property
+    def block_bytes(self) -> int:
+        return self.info().block_bytes
+
+    @property
+    def table_bytes(self) -> int:
+        return self.info().table_bytes
+
+    def read_words(self, off: int, count: int) -> np.ndarray:
+        return self._main.read_words(off, count)
 
     def crt_capable(self) -> bool:
         """Whether the key owner's encryption goes by CRT (crt_keys): the private key factors n
         (p q = n, p != q), half-length primes of a supported limb class, EFL_PL_CRT_ENCRYPT not 0."""
-        if not self.desc.has_private or os.environ.get("EFL_PL_CRT_ENCRYPT", "1") == "0":
-            return False
-        if self.p == self.q or self.p * self.q != self.n:
-            return False
-        for x in (self.p, self.q):
-            ln_x = next((c for c in _LIMB_CLASSES if 32 * c >= x.bit_length()), None)
-            if ln_x is None or 2 * ln_x != self.ln:
-                return False
-        return True
+        return bool(self.info().crt_capable)
+
+    def ensure_table(self):
+        """Build the n^2 fixed-base table if this key has none yet (the key owner's is deferred:
+        its encryptions go by CRT). Returns self."""
+        with torch.cuda.device(self.device):
+            _efl_lib.check(min(0, _lib.efl_pl_ctx_prepare(self.ctx, PREPARE_TABLE, _stream(self.device))))
+        return self
 
     def crt_keys(self):
-        """The key owner's encryption keys: (KeyBlock of (p, hs mod p^2), KeyBlock of (q, hs mod
-        q^2)), built on first use. hs^(a') mod n^2 is then two fixed-base exponentiations on
-        half-length moduli (a quarter of the limb products each) and one CRT join
-        (efl_pl_crt_join): the same value, bit for bit, as the public-key path. None without the
-        private key, with EFL_PL_CRT_ENCRYPT=0, or when p and q are not half-length primes of a
-        supported limb class (512-bit n: 256-bit primes). Also None when the private key does not
-        factor n (p q != n, or p == q): the reference's Encrypt works mod n^2 only, so such a key
-        still encrypts correctly there (paillier.cc:103-131), and the public-key path keeps that."""
-        if self._crt is None:
-            self._crt = False
-            if self.crt_capable():
-                subs = []
-                p2, q2 = self.p * self.p, self.q * self.q
-                R = 1 << (32 * self.lc)   # the n^2 Montgomery radix: the join yields hsa R (efl_pl_crt_join)
-                for x, start in ((self.p, R * pow(q2, -1, p2)), (self.q, R * pow(p2, -1, q2))):
-                    # the walk mod p^2 yields hs^(a') R (q^2)^-1, mod q^2 hs^(a') R (p^2)^-1: the join
-                    # v = q^2 yp + p^2 yq mod n^2 = hs^(a') R then needs no modular product, and
-                    # g(m) hs^(a') = mont(g(m), v) is one. The two sub-tables share the keypair's
-                    # budget (half each); the key owner's n^2 table is deferred (ensure_table)
-                    subs.append(KeyBlock(x, self.hs % (x * x), self.a_bits, self.group_size, device=self.device,
-                                         walk_start=start, table_window=self._window_arg,
-                                         max_bytes=self._max_bytes // 2, defer_table=False))
-                self._crt = tuple(subs)
-        return self._crt or None
-
-    def _build_table(self, hs, n2, W, rows, cols, head, r_one, L28, chunk_bytes=64 << 20):
-        """T[i][j-1] = hs^(j 2^(W i)) mod n^2 for j in 1..2^W-1, in Montgomery form (x R mod n^2,
-        [rows, cols, 2 ln] words) and, with L28, radix-2^28 Montgomery form (x R28 mod n^2,
-        [rows, cols, L28] limbs): the table the reference fills with one mpz_mul per entry when a
-        keypair is set (gmp_utils.cc:73-88), built here with one GPU product per entry as well.
-        One native host call gives every hs^(2^t), t < W rows (efl_host_sqr_chain): P[i][k] =
-        b_i^(2^k) for the row base b_i = hs^(2^(W i)). Column 1 is b_i R; pass k then fills columns
-        2^k + 1 .. 2^(k+1) of every row at once as column i times P[i][k] (efl_pl_add, which
-        multiplies mod n^2: x R * y = x y R), so W passes of independent products replace a chain
-        per row. Round 3 ran an efl_pl_powm of b_i^j per entry (about 1.5 W products each). The
-        radix-2^28 copy is x R times R28 R^-1 (one more product) cut into 28-bit limbs. Launches
-        move at most chunk_bytes of entries."""
-        dev, lc = self.device, self.lc
-        sh = _stream(dev)
-        d = self.desc
-        ptr, dp = head.data_ptr(), ctypes.byref(d)
-
-        def mul(dst, a, b, N):
-            _efl_lib.check(_lib.efl_pl_add(ptr, dp, a.data_ptr(), b.data_ptr(), dst.data_ptr(), N, sh))
-
-        P = torch.from_numpy(host_sqr_chain(hs, 1, rows * W, n2, lc).view(np.int32)).to(dev).reshape(rows, W, lc)
-        t32 = torch.empty((rows, cols, lc), dtype=torch.int32, device=dev)
-        ce = max(1, chunk_bytes // (4 * lc))              # entries per launch
-        col = torch.empty((rows, lc), dtype=torch.int32, device=dev)
-        mul(col, P[:, 0].contiguous(), head[r_one:r_one + lc].expand(rows, lc).contiguous(), rows)
-        t32[:, 0] = col
-        for k, (lo, cnt) in enumerate(table_passes(W, cols)):
-            if cnt >= ce:                                 # long rows: slices of one row, in place
-                for r in range(rows):
-                    for c0 in range(0, cnt, ce):
-                        c1 = min(cnt, c0 + ce)
-                        m = P[r, k].expand(c1 - c0, lc).contiguous()
-                        mul(t32[r, lo + c0:lo + c1], t32[r, c0:c1], m, c1 - c0)
-            else:                                         # short rows: several rows per launch
-                rb = max(1, ce // cnt)
-                for r0 in range(0, rows, rb):
-                    r1 = min(rows, r0 + rb)
-                    src = t32[r0:r1, :cnt].contiguous()
-                    m = P[r0:r1, k:k + 1].expand(r1 - r0, cnt, lc).contiguous()
-                    out = torch.empty_like(src)
-                    mul(out, src, m, (r1 - r0) * cnt)
-                    t32[r0:r1, lo:lo + cnt] = out
-        if not L28:
-            return t32, None
-        t28 = torch.empty((rows, cols, L28), dtype=torch.int32, device=dev)
-        R, R28 = 1 << (32 * lc), 1 << (28 * L28)
-        c28 = torch.from_numpy(_limbs(R28 * pow(R, -1, n2) % n2, lc).view(np.int32)).to(dev)
-        q, r = divmod(np.arange(L28) * 28, 32)
-        qi = torch.from_numpy(q).to(dev)
-        rs = torch.from_numpy(r).to(dev)
-        pad = int(q.max()) + 2 - lc                       # x R28 mod n^2 < 2^(32 lc): words past lc are 0
-        flat32, flat28 = t32.reshape(-1, lc), t28.reshape(-1, L28)
-        total = rows * cols
-        ce28 = max(1, ce // 4)                            # the int64 staging below is 4x the entries
-        for e0 in range(0, total, ce28):
-            e1 = min(total, e0 + ce28)
-            N = e1 - e0
-            X = torch.empty((N, lc), dtype=torch.int32, device=dev)
-            mul(X, flat32[e0:e1], c28.expand(N, lc).contiguous(), N)
-            w = torch.cat([X.to(torch.int64) & 0xFFFFFFFF,
-                           torch.zeros((N, max(1, pad)), dtype=torch.int64, device=dev)], dim=1)
-            flat28[e0:e1] = (((w[:, qi] >> rs) | (w[:, qi + 1] << (32 - rs))) & 0xFFFFFFF).to(torch.int32)
-        return t32, t28
-
-    def args(self):
-        return self.ptr, ctypes.byref(self.desc)
+        """The key owner's encryption keys ((p, hs mod p^2) and (q, hs mod q^2), walks starting from
+        R (q^2)^-1 and R (p^2)^-1) as key views, built on first use; None when this key cannot take
+        them (no private key, p q != n, p == q, primes not of a half-length limb class, CRT off, or
+        no room in the table budget). The reference's Encrypt works mod n^2 only
+        (paillier.cc:103-131); the join gives its ciphertexts bit for bit."""
+        with torch.cuda.device(self.device):
+            rc = _lib.efl_pl_ctx_prepare(self.ctx, PREPARE_CRT, _stream(self.device))
+        _efl_lib.check(min(0, rc))
+        if rc != 1:
+            return None
+        gen = self.info().generation
+        if self._crt_views is None or self._crt_views[0] != gen:
+            self._crt_views = (gen, (_KeyView(self, 1, self.p, self.lh), _KeyView(self, 2, self.q, self.lh)))
+        return self._crt_views[1]
 
 
 # ----------------------------------------------------------------------------------------------
@@ -798,29 +718,36 @@ class PaillierKeypair(object):
         self._set(int(_hex_of(n), 16), _int_of(n_bytes), int(_hex_of(hs), 16), _int_of(a_bytes), 1)
 
     def set_private_key(self, p, q):
-        """SetPaillierPrivateKey (ignored without a public key, paillier.cc:88-91)."""
+        """SetPaillierPrivateKey (ignored without a public key, paillier.cc:88-91): in place, the
+        public key and its table stay (efl_pl_set_private)."""
         if self._key is None:
             return
-        k = self._key
-        self._set(k.n, self._n_bytes, k.hs, k.a_bits // 8, k.group_size,
-                  int(_hex_of(p), 16), int(_hex_of(q), 16))
+        self._key.set_private(int(_hex_of(p), 16), int(_hex_of(q), 16))
 
     def set_keys_ints(self, n, hs, a_bytes, group_size=1, p=None, q=None, n_bytes=None, table_window=None):
         """Host-int variant of set_public_key/set_private_key (tests, key exchange). table_window
-        forces the fixed-base table's window (default: choose_table_window; results never change)."""
+        forces the fixed-base table's window (default: chosen against the table budget; results
+        never change)."""
         self._set(n, n_bytes or (n.bit_length() + 7) // 8, hs, a_bytes, group_size, p, q, table_window)
 
     def _set(self, n, n_bytes, hs, a_bytes, group_size, p=None, q=None, table_window=None):
         old = self._key
-        if old is not None and (old.n, old.hs) != (n, hs):
-            # a new public key (a re-key): nothing of the old block can be reused, so the keypair
-            # lets go of it, and of the key owner's CRT sub-tables, before the new table is built.
-            # Ciphertexts that still reference the old block keep it alive; its sub-tables only
-            # ever served this keypair's own encryptions.
-            old._crt = None
-            self._key = old = None
-        self._key = KeyBlock(n, hs, 8 * int(a_bytes), int(group_size), p, q, table_window=table_window,
-                             reuse_table=old)
+        a_bits = 8 * int(a_bytes)
+        if old is not None and p is not None and q is not None and table_window is None \
+                and (old.n, old.hs, old.a_bits, old.group_size) == (n, hs, a_bits, int(group_size)):
+            old.set_private(p, q)        # the same public key: its table stays
+            self._n_bytes = n_bytes
+            return
+        if old is not None:
+            # a re-key: the new key is checked on the host first, so a refused key (bad argument,
+            # unsupported size, the reference's table guard) leaves the old one in place; then the
+            # old key's device memory is let go of before the new tables are sized against the
+            # process-wide budget. Ciphertexts made under the old key keep their limbs; their key
+            # handle is closed (every op takes the keypair's current key, as the reference's do).
+            KeyBlock.check(n, hs, a_bits, int(group_size), p, q, table_window)
+            self._key = None
+            old.close()
+        self._key = KeyBlock(n, hs, a_bits, int(group_size), p, q, table_window=table_window, n_bytes=n_bytes)
         self._n_bytes = n_bytes
 
     @property
@@ -846,29 +773,15 @@ class PaillierKeypair(object):
         return CipherTensor(limbs, hx.shape, k)
 
     # -- ops -----------------------------------------------------------------------------
-    def _crt_encrypt(self, m, n, counter_base, a_dev=None):
-        """The key owner's path (KeyBlock.crt_keys): ciphertexts of the int64 device tensor m ([n, 2 ln]
-        limbs) for the Philox draws at counters counter_base + i (or the given exponents a_dev) —
-        m = 0 gives hs^(a') itself. None when this keypair cannot take it."""
-        k = self.key
-        subs = k.crt_keys() if self.crt_encrypt else None
-        if subs is None or n == 0:
-            return None
-        sh = _stream(k.device)
-        parts = []
-        for sk in subs:
-            x = torch.empty((n, sk.lc), dtype=torch.int32, device=k.device)
-            _efl_lib.check(_lib.efl_pl_fbpowm(*sk.args(), a_dev.data_ptr() if a_dev is not None else None,
-                                              x.data_ptr(), n, self.seed, counter_base, sh))
-            parts.append(x)
-        z = torch.empty((n, k.lc), dtype=torch.int32, device=k.device)
-        _efl_lib.check(_lib.efl_pl_crt_join(*k.args(), parts[0].data_ptr(), parts[1].data_ptr(), m.data_ptr(),
-                                            z.data_ptr(), n, sh))
-        return z
+    def _path_flags(self) -> int:
+        """efl_pl_ctx_encrypt / _fbpowm flags: the key owner's CRT path unless crt_encrypt is off."""
+        return 0 if self.crt_encrypt else PUBLIC_PATH
 
     def encrypt(self, plaintext, hsa=None, counter_base=None):
         """PaillierEncrypt (paillier.cc:443-503). hsa None (or all "0") draws a fresh a per element
-        from Philox(seed, counter); counter_base defaults to a running per-keypair counter."""
+        from Philox(seed, counter); counter_base defaults to a running per-keypair counter. The key
+        context routes it (efl_pl_ctx_encrypt): the key owner by CRT, a public-key holder through
+        the n^2 table, a given hsa straight to the product; the same ciphertexts on every path."""
         k = self.key
         m = _efl_lib.as_tensor(plaintext)
         if m.dtype != torch.int64:
@@ -892,15 +805,10 @@ class PaillierKeypair(object):
         ctr = self.counter if counter_base is None else int(counter_base)
         if counter_base is None:
             self.counter += N
-        crt = self._crt_encrypt(m, N, ctr) if hsa_limbs is None else None   # the key owner: by CRT, same bits
-        if crt is not None:
-            out = crt
-        else:
-            if hsa_limbs is None:
-                k.ensure_table()          # fresh randomness walks the n^2 table
-            _efl_lib.check(_lib.efl_pl_encrypt(*k.args(), m.data_ptr(),
+        sh, fl = _stream(k.device), self._path_flags()
+        _efl_lib.check(_lib.efl_pl_ctx_encrypt(k.ctx, m.data_ptr(),
                                                hsa_limbs.data_ptr() if hsa_limbs is not None else None,
-                                               out.data_ptr(), N, self.seed, ctr, _stream(k.device)))
+                                               out.data_ptr(), N, self.seed, ctr, fl, sh))
         if hsa_limbs is not None and zero_idx is not None and zero_idx.size:
             # the rows whose hsa is "0" draw a fresh a at their own index's counter (ctr + idx),
             # inside this call's range: rows with a given hsa consume no counter
@@ -908,13 +816,8 @@ class PaillierKeypair(object):
             sub = torch.empty((idx.numel(), k.lc), dtype=torch.int32, device=k.device)
             msub = m[idx].contiguous()
             for j0, j1, c0 in _counter_runs(zero_idx):
-                h = self._crt_encrypt(msub[j0:j1], j1 - j0, ctr + c0)
-                if h is not None:
-                    sub[j0:j1] = h
-                    continue
-                k.ensure_table()
-                _efl_lib.check(_lib.efl_pl_encrypt(*k.args(), msub[j0:j1].data_ptr(), None, sub[j0:j1].data_ptr(),
-                                                   j1 - j0, self.seed, ctr + c0, _stream(k.device)))
+                _efl_lib.check(_lib.efl_pl_ctx_encrypt(k.ctx, msub[j0:j1].data_ptr(), None, sub[j0:j1].data_ptr(),
+                                                       j1 - j0, self.seed, ctr + c0, fl, sh))
             out[idx] = sub
         return PaillierTensor(self, CipherTensor(out, shape, k))
 
@@ -930,6 +833,7 @@ class PaillierKeypair(object):
         else:
             counter_base = 0
         words = (k.a_bits + 31) // 32
+        a_dev = None
         if a is not None:
             a = list(a)
             n = len(a)
@@ -937,27 +841,23 @@ class PaillierKeypair(object):
                 raise errors.InvalidArgumentError("exponent wider than the fixed-base table")
             arr = np.stack([_limbs(v, words) for v in a]) if n else np.zeros((0, words), "<u4")
             a_dev = torch.from_numpy(arr.view(np.int32)).to(k.device)
-        zeros = torch.zeros(n, dtype=torch.int64, device=k.device)   # g(0) = 1: the join gives hs^(a')
-        out = self._crt_encrypt(zeros, n, counter_base, a_dev if a is not None else None)
-        if out is None:
-            out = torch.empty((n, k.lc), dtype=torch.int32, device=k.device)
-            k.ensure_table()
-            _efl_lib.check(_lib.efl_pl_fbpowm(*k.args(), a_dev.data_ptr() if a is not None else None,
-                                              out.data_ptr(), n, self.seed, counter_base, _stream(k.device)))
+        out = torch.empty((n, k.lc), dtype=torch.int32, device=k.device)
+        _efl_lib.check(_lib.efl_pl_ctx_fbpowm(k.ctx, a_dev.data_ptr() if a_dev is not None else None, out.data_ptr(),
+                                              n, self.seed, counter_base, self._path_flags(), _stream(k.device)))
         return CipherTensor(out, (n,), k)
 
     def decrypt(self, paillier_tensor, dtype="string"):
         """PaillierDecrypt (paillier.cc:505-561): HexTensor of the signed plaintext (default) or
         int64 (mpz_get_sll semantics)."""
         k = self.key
-        if not k.desc.has_private:
+        if k.p is None:
             raise errors.AbortedError("No private key.")
         c = self._cipher(paillier_tensor)
         N = c.numel()
         mag = torch.empty((N, k.ln), dtype=torch.int32, device=k.device)
         neg = torch.empty(N, dtype=torch.int8, device=k.device)
-        _efl_lib.check(_lib.efl_pl_decrypt(*k.args(), c.limbs.data_ptr(), mag.data_ptr(), neg.data_ptr(), N,
-                                           _stream(k.device)))
+        _efl_lib.check(_lib.efl_pl_ctx_decrypt(k.ctx, c.limbs.data_ptr(), mag.data_ptr(), neg.data_ptr(), N,
+                                               _stream(k.device)))
         if _is_string_dtype(dtype):
             return limbs_to_hex(mag, neg, c.shape)
         if _efl_lib.to_torch_dtype(dtype) != torch.int64:

@@ -316,6 +316,100 @@ int efl_pl_matmul(const void* key_block, const efl_pl_key* key, const uint32_t* 
  * at most v), -1 queries. */
 int efl_pl_tune(int ln, int decrypt, int limbs_per_lane);
 
+/* ---- Key context: the PaillierKeypair resource ----------------------------------------------
+ * Replaces CreatePaillierKeypair / SetPaillierPublicKey / SetPaillierPrivateKey
+ * (efls-train/cc/efl/math/paillier.cc:337-441; PaillierKeypair::SetPublicKey / SetPrivateKey
+ * :70-101; the fixed-base table of gmp_utils.cc:56-89) and the Python binding's
+ * Keypair.set_public_key / set_private_key (python/efl/privacy/paillier.py:62-73). An opaque
+ * context holds the key block(s) above in device memory, derived by the library from the hex text
+ * (csrc/keyset.hip): the caller packs nothing. A TF shim keeps one context per keypair resource.
+ *
+ * Device memory of the fixed-base tables is budgeted PROCESS-WIDE (efl_pl_table_budget; default
+ * 4 GiB, EFL_PL_TABLE_BUDGET_MIB) and per context (efl_pl_ctx_options; default 4 GiB,
+ * EFL_PL_TABLE_MAX_MIB): a key's table takes the widest window whose table fits what is left; when
+ * not even the smallest (W = 1) does, or the reference's own guard trips (entries x bits of n^2 of
+ * the table IT would build > 2^40, gmp_utils.h:20), setting the key returns RESOURCE_EXHAUSTED
+ * "Memory usage exceeds a predefined threshold." (paillier.cc:399-401). A refused key leaves the
+ * context's previous key in place. Setting a key synchronises `stream` (a one-off host op, like the
+ * reference's synchronous SetPublicKey). */
+typedef struct efl_pl_ctx efl_pl_ctx;
+
+enum {
+  EFL_PL_PREPARE_TABLE = 1,   /* efl_pl_ctx_prepare: build the n^2 fixed-base table now */
+  EFL_PL_PREPARE_CRT = 2,     /* build the key owner's CRT sub-keys now */
+  EFL_PL_PUBLIC_PATH = 1      /* efl_pl_ctx_encrypt / _fbpowm flag: walk the n^2 table even for the key owner */
+};
+
+typedef struct {
+  int32_t has_public, has_private, n_bytes, ln, a_bits, group_size;
+  int32_t table_window;           /* of the n^2 table (planned, if not built yet) */
+  int32_t has_table;              /* the n^2 table is built (the key owner's is deferred) */
+  int32_t crt_capable;            /* p q = n with half-length primes, CRT encryption enabled */
+  int32_t crt;                    /* 1 sub-keys built, 0 not tried, -1 not available (budget) */
+  int32_t crt_table_window[2];
+  int64_t block_bytes, table_bytes, table_max_bytes;
+  int64_t crt_block_bytes[2], crt_table_bytes[2];
+  uint64_t generation;            /* changes whenever a pointer efl_pl_ctx_key gave may have */
+} efl_pl_ctx_info;
+
+/* CreatePaillierKeypair: an empty context. */
+int efl_pl_ctx_create(efl_pl_ctx** ctx);
+/* Frees every device block (hipFree: waits for work that still reads them). */
+int efl_pl_ctx_destroy(efl_pl_ctx* ctx);
+/* Options for the next key set on ctx: table_max_bytes (-1: EFL_PL_TABLE_MAX_MIB or 4 GiB, -2
+ * unchanged), table_window (1..24 fixed, 0 chosen against the budget, -1 unchanged; results never
+ * depend on it), crt_encrypt (1 on, 0 off, -1 EFL_PL_CRT_ENCRYPT (default on), -2 unchanged). */
+int efl_pl_ctx_options(efl_pl_ctx* ctx, int64_t table_max_bytes, int table_window, int crt_encrypt);
+/* SetPaillierPublicKey(n, n_bytes, hs, a_bytes, group_size): hex texts (NUL-terminated,
+ * mpz_set_str base 16). Drops any private key (paillier.cc:79). The n^2 table is built now unless
+ * the key is later made a key owner's. */
+int efl_pl_set_public(efl_pl_ctx* ctx, const char* n_hex, int n_bytes, const char* hs_hex, int a_bytes,
+                      int group_size, void* stream);
+/* Both halves at once (GeneratePaillierKeypair's final step, paillier.cc:889-904): the key owner's
+ * n^2 table is then deferred from the start (its encryptions go by CRT). */
+int efl_pl_set_keypair(efl_pl_ctx* ctx, const char* n_hex, int n_bytes, const char* hs_hex, int a_bytes,
+                       int group_size, const char* p_hex, const char* q_hex, void* stream);
+/* SetPaillierPrivateKey(p, q): ignored without a public key (paillier.cc:88-91). p, q distinct odd
+ * (INVALID_ARGUMENT otherwise, where the reference's mpz_invert would fail silently). */
+int efl_pl_set_private(efl_pl_ctx* ctx, const char* p_hex, const char* q_hex, void* stream);
+/* The key block and descriptor every efl_pl_* op above takes: which 0 = the key, 1 / 2 = the key
+ * owner's CRT sub-keys (p, hs mod p^2) / (q, hs mod q^2) (after EFL_PL_PREPARE_CRT). ABORTED "No
+ * public key." without one. Valid until the next set / prepare / destroy on ctx (see generation). */
+int efl_pl_ctx_key(efl_pl_ctx* ctx, int which, const void** block, efl_pl_key* key);
+/* Build what a path needs ahead of use: EFL_PL_PREPARE_TABLE -> 1 (or RESOURCE_EXHAUSTED);
+ * EFL_PL_PREPARE_CRT -> 1 sub-keys ready, 0 this key cannot take them (no private key, p q != n, no
+ * room in the budget, CRT off). */
+int efl_pl_ctx_prepare(efl_pl_ctx* ctx, int what, void* stream);
+int efl_pl_ctx_query(efl_pl_ctx* ctx, efl_pl_ctx_info* info);
+/* Copy count 32-bit words of block `which` from word off_words into dst (device or host memory). */
+int efl_pl_ctx_copy(efl_pl_ctx* ctx, int which, int64_t off_words, int64_t count, void* dst, void* stream);
+/* PaillierEncrypt through the context: hsa given -> efl_pl_encrypt; otherwise the key owner's CRT
+ * path (sub-keys' walks + efl_pl_crt_join) unless flags has EFL_PL_PUBLIC_PATH, else the n^2 table
+ * (built on first use). Same ciphertexts, bit for bit, on every path. The CRT path takes
+ * stream-ordered scratch (2 n ln words). */
+int efl_pl_ctx_encrypt(efl_pl_ctx* ctx, const int64_t* plaintext, const uint32_t* hsa, uint32_t* ciphertext,
+                       int64_t n, uint64_t seed, int64_t counter_base, int flags, void* stream);
+/* FixedBasePowm through the context (hs^(a') mod n^2; a NULL = the Philox draw), routed as above. */
+int efl_pl_ctx_fbpowm(efl_pl_ctx* ctx, const uint32_t* a, uint32_t* hsa, int64_t n, uint64_t seed,
+                      int64_t counter_base, int flags, void* stream);
+/* PaillierDecrypt through the context: ABORTED "No private key." without p, q. */
+int efl_pl_ctx_decrypt(efl_pl_ctx* ctx, const uint32_t* ciphertext, uint32_t* magnitude, int8_t* negative,
+                       int64_t n, void* stream);
+/* Process-wide table budget in bytes: bytes >= 0 sets it, < 0 only queries; returns the previous
+ * budget; in_use (optional) <- bytes the live contexts' tables hold. */
+int64_t efl_pl_table_budget(int64_t bytes, int64_t* in_use);
+/* The window rule: widest W <= 24 with ceil(a_bits / W) (2^W - 1) entry_bytes <= max_bytes, 0 if
+ * none. */
+int efl_pl_choose_window(int a_bits, int64_t entry_bytes, int64_t max_bytes);
+
+/* The host half of setting a key, without the device (tests, inspection): the head words of the key
+ * block (the constants, before any table) and its descriptor, for n, hs (and p, q; and a walk start
+ * w: the fixed-base walk then starts from w R instead of R, as the CRT sub-keys do), with the table
+ * plan (table_rows = rows it will have; off_table = -1). head NULL: *head_words <- the size only. */
+int efl_pl_key_derive(const char* n_hex, const char* hs_hex, int a_bytes, int group_size, const char* p_hex,
+                      const char* q_hex, const char* walk_hex, int table_window, int64_t allowance,
+                      uint32_t* head, int64_t* head_words, efl_pl_key* desc);
+
 /* mpz_get_str(..., 16) of n numbers ([n][limbs_per_elem], optional sign bytes): first the text
  * lengths (efl_hex_lengths), then, given offsets = exclusive prefix sum (n + 1 entries), the
  * characters (efl_hex_write). */

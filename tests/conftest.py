@@ -19,6 +19,9 @@ def pytest_configure(config):
     # 3.8 GB table for a 512-bit test key) would only slow their setup. Tests run with round 3's
     # 1.5 GiB unless they set the budget themselves (results never depend on the table's window).
     os.environ.setdefault("EFL_PL_TABLE_MAX_MIB", "1536")
+    # the process-wide budget (default 4 GiB) would make a test's window depend on the keypairs
+    # earlier tests still hold; tests of the budget itself set it through efl_pl_table_budget
+    os.environ.setdefault("EFL_PL_TABLE_BUDGET_MIB", "65536")
     # build the oracle (CPU checker) and the HIP library if they are missing; an existing library
     # is never rebuilt here (tests/test_abi.py::test_library_built_from_this_tree fails if it is
     # stale), so a GPU run uses exactly the .so that was pushed with the tree

@@ -90,6 +90,7 @@ def party_rotation(role, kind, my, peer, q):
     installs it. Records per step: the key's n, device memory around the re-key, the layer values."""
     try:
         import efl
+        from efl.privacy import paillier_cipher as pc      # table bytes live outside torch's allocator
         Role = efl.privacy.Role
         g = torch.Generator().manual_seed(12)
         units = 4
@@ -105,12 +106,12 @@ def party_rotation(role, kind, my, peer, q):
         rec = []
         for step in range(ROT_STEPS):
             torch.cuda.synchronize()
-            m0 = torch.cuda.memory_allocated()
+            m0 = torch.cuda.memory_allocated() + pc.table_budget()[1]
             old = weakref.ref(kp.key) if step else None
             model.begin_step()                        # re-key on steps 0, 2, 4
             torch.cuda.synchronize()
-            m1 = torch.cuda.memory_allocated()
-            key_bytes = kp.key.block.numel() * 4
+            m1 = torch.cuda.memory_allocated() + pc.table_budget()[1]
+            key_bytes = kp.key.block_bytes
             rekeyed = old is not None and old() is not kp.key
             old_alive = rekeyed and old() is not None
             if sender:
@@ -129,7 +130,7 @@ def party_rotation(role, kind, my, peer, q):
                 vals = (before, W.detach().cpu().clone(), y.detach().cpu(), dy.cpu())
                 del y, loss, dy
             subs = kp.key.crt_keys() if sender else None
-            crt_bytes = sum(s.block.numel() * 4 for s in subs) if subs else 0
+            crt_bytes = sum(s.block_bytes for s in subs) if subs else 0
             model.end_step()
             rec.append(dict(n=kp.key.n, m0=m0, m1=m1, key_bytes=key_bytes, crt_bytes=crt_bytes, rekeyed=rekeyed,
                             old_alive=old_alive,

@@ -355,6 +355,46 @@ def test_batched_embedding_slices(efl):
         assert np.array_equal(host(Ms[i]), Mo) and np.array_equal(host(Es[i]), Eo)
 
 
+@pytest.mark.parametrize("coalesce", ["single", True])
+def test_batched_config3_separate_full_size(efl, coalesce):
+    """BASELINE config 3 exactly as bench.py's `config3` (layout "separate") builds it: 4096
+    [128, 128] fp32 slices, N(0, 0.01), seed 1, every slice and every output its own allocation.
+    coalesce="single" (the default) keeps one table entry per slice, so the batched kernels
+    (efl_fxp_encode_batched / efl_fxp_decode_batched) run with count = 4096; True merges the
+    runs the caching allocator happened to lay out back to back. Every element of all 4096 slices
+    is compared bit for bit with the oracle (fixed_point.cc:106-138 encode, :235-248 decode, FTZ)."""
+    slices = 4096
+    g = torch.Generator(device="cuda").manual_seed(1)
+    xs = [torch.randn(128, 128, device="cuda", generator=g) * 0.01 for _ in range(slices)]
+    Ms = [torch.empty(128, 128, dtype=torch.int64, device="cuda") for _ in range(slices)]
+    Es = [torch.empty(128, 128, dtype=torch.int64, device="cuda") for _ in range(slices)]
+    ys = [torch.empty(128, 128, device="cuda") for _ in range(slices)]
+    enc = efl.lib.BatchTables(xs, Ms, Es, coalesce=coalesce)
+    dec = efl.lib.BatchTables(Ms, Es, ys, coalesce=coalesce)
+    assert not enc.single and not dec.single
+    if coalesce == "single":
+        assert enc.count == slices and dec.count == slices
+    else:
+        assert 1 < enc.count < slices and 1 < dec.count < slices
+    for t in (enc, dec):
+        assert t.max_n == max(r[3] for r in t.runs)
+    efl.lib.encode_batched_into(enc, 1, False)
+    efl.lib.decode_batched_into(dec, 1, 1)
+    torch.cuda.synchronize()
+    x_h = host(torch.stack(xs)).reshape(-1)
+    Mo, Eo = fxp.encode(x_h)
+    M_h, E_h = host(torch.stack(Ms)).reshape(-1), host(torch.stack(Es)).reshape(-1)
+    bad = np.nonzero((M_h != Mo) | (E_h != Eo))[0]
+    assert bad.size == 0, f"encode differs at {bad.size} elements, first {bad[:4]} (slice {bad[0] // 16384})"
+    yo = fxp.decode(Mo, Eo, ftz=True).view(np.uint32)
+    y_h = bits32(torch.stack(ys)).reshape(-1)
+    bad = np.nonzero(y_h != yo)[0]
+    assert bad.size == 0, f"decode differs at {bad.size} elements, first {bad[:4]}"
+    # per-slice checksums (a second, order-sensitive view of the same comparison)
+    ck = lambda a: (a.reshape(slices, -1).astype(np.uint64) * np.arange(1, 16385, dtype=np.uint64)).sum(1)
+    assert np.array_equal(ck(M_h.view(np.uint64)), ck(Mo.view(np.uint64)))
+
+
 @pytest.mark.parametrize("coalesce", ["single", True, False])
 def test_batched_tables_coalescing_identical(efl, coalesce):
     """BatchTables over slices of one table: as one run through the streaming kernels ("single",

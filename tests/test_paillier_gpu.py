@@ -149,46 +149,51 @@ def _as_ints(words, width, bits):
 
 
 @pytest.mark.parametrize("W", [1, 2, 5, 7])
-def test_table_built_on_gpu_matches_host(efl, W):
-    """The fixed-base table efl builds on the GPU (every hs^(2^t) on the host, then column 1 = b R
-    and W passes of one efl_pl_add product per entry, then x R28 by one more) equals
-    hs^(j 2^(W i)) R mod n^2 computed with Python ints, every entry of both layouts; and so does a
-    build whose launches take 8 entries (the per-row path of the long passes)."""
+def test_table_built_on_gpu_matches_host(efl, W, monkeypatch):
+    """The fixed-base table the key context builds on the GPU (csrc/keyset.hip: every hs^(2^t) on
+    the host, then column 1 = b R and W passes of one efl_pl_add product per entry, then x R28 by one
+    more) equals hs^(j 2^(W i)) R mod n^2 computed with Python ints, every entry of both layouts; and
+    so does a build whose launches take 8 entries each (EFL_PL_TABLE_CHUNK_BYTES)."""
     from efl.privacy import paillier_cipher as pc
     k = ENC_KEYS[1]
     n, hs = int(k["n"], 16), int(k["hs"], 16)
-    kb = pc.KeyBlock(n, hs, k["a_bits"], 1, table_window=W)
-    d = kb.desc
     n2 = n * n
-    rows, cols, lc = d.table_rows, d.table_cols, kb.lc
-    want = [v for row in _host_table(hs, n2, W, rows, cols, 1 << (32 * lc)) for v in row]
-    blk = kb.block.cpu().numpy().view(np.uint32)
-    assert _as_ints(blk[d.off_table:d.off_table + rows * cols * lc], lc, 32) == want
-    L28 = d.n2_28_len if d.off_table28 >= 0 else 0
-    assert L28
-    inv = pow(1 << (32 * lc), -1, n2) * (1 << (28 * L28))
-    want28 = [v * inv % n2 for v in want]
-    assert _as_ints(blk[d.off_table28:d.off_table28 + rows * cols * L28], L28, 28) == want28
-    W_, rows_, cols_, L28_, r_one, _, _ = kb._tab
-    t32, t28 = kb._build_table(hs % n2, n2, W_, rows_, cols_, kb._head, r_one, L28_, chunk_bytes=8 * 4 * lc)
-    assert torch.equal(t32.reshape(-1), kb.block[d.off_table:d.off_table + rows * cols * lc])
-    assert torch.equal(t28.reshape(-1), kb.block[d.off_table28:d.off_table28 + rows * cols * L28])
+    for chunk in (None, 8 * 4 * 64):
+        if chunk:
+            monkeypatch.setenv("EFL_PL_TABLE_CHUNK_BYTES", str(chunk))
+        kb = pc.KeyBlock(n, hs, k["a_bits"], 1, table_window=W)
+        d = kb.desc
+        rows, cols, lc = d.table_rows, d.table_cols, kb.lc
+        assert lc == 64
+        want = [v for row in _host_table(hs, n2, W, rows, cols, 1 << (32 * lc)) for v in row]
+        assert _as_ints(kb.read_words(d.off_table, rows * cols * lc), lc, 32) == want
+        L28 = d.n2_28_len if d.off_table28 >= 0 else 0
+        assert L28
+        inv = pow(1 << (32 * lc), -1, n2) * (1 << (28 * L28))
+        want28 = [v * inv % n2 for v in want]
+        assert _as_ints(kb.read_words(d.off_table28, rows * cols * L28), L28, 28) == want28
+        assert kb.table_bytes == rows * cols * (lc + L28) * 4
+        kb.close()
 
 
 @pytest.mark.parametrize("k", ALL, ids=ids)
 def test_default_table_window_keeps_the_radix28_table(efl, k, monkeypatch):
-    """The default window (the widest whose table, both layouts, fits the 4 GiB budget) keeps the
+    """The default window (the widest whose table, both layouts, fits the 4 GiB cap) keeps the
     radix-2^28 copy the n^2 kernels walk (profiles/r04/table_window_*)."""
     from efl.privacy import paillier_cipher as pc
-    monkeypatch.delenv("EFL_PL_TABLE_MAX_MIB", raising=False)     # the production budget
+    monkeypatch.delenv("EFL_PL_TABLE_MAX_MIB", raising=False)     # the production cap
     n, hs = int(k["n"], 16), int(k["hs"], 16)
+    budget, used = pc.table_budget()
+    assert budget - used >= pc.TABLE_MAX_BYTES                    # the session's budget leaves the cap binding
     kb = pc.KeyBlock(n, hs, k["a_bits"], 1)
     assert kb.has_table
     want = {512: 20, 1024: 18, 2048: 15, 4096: 13}[8 * k["n_bytes"]]
     assert kb.table_window == want
     if pc.kernel_slicing(kb.ln, False):
         assert kb.desc.off_table28 >= 0
-    assert kb.block.numel() * 4 <= pc.table_max_bytes() + (64 << 20)   # the table plus the key's constants
+    assert kb.table_bytes <= pc.table_max_bytes()
+    assert kb.block_bytes <= pc.table_max_bytes() + (1 << 20)   # the table plus the key's constants
+    kb.close()
 
 
 @pytest.mark.parametrize("k,c", fams(ALL))

@@ -45,8 +45,8 @@ def main():
             subs = kp.key.crt_keys() or ()
             gen.append({"keygen_s": round(t1 - t0, 3), "key_block_s": round(t2 - t1, 3),
                         "crt_subkeys_s": round(t3 - t2, 3),
-                        "table_MiB": round(kp.key.block.numel() * 4 / MIB, 1),
-                        "crt_tables_MiB": round(sum(s.block.numel() for s in subs) * 4 / MIB, 1),
+                        "table_MiB": round(kp.key.block_bytes / MIB, 1),
+                        "crt_tables_MiB": round(sum(s.block_bytes for s in subs) / MIB, 1),
                         "held_before_MiB": round((before - base) / MIB, 1),
                         "held_after_MiB": round((torch.cuda.memory_allocated(dev) - base) / MIB, 1),
                         "peak_MiB": round((torch.cuda.max_memory_allocated(dev) - base) / MIB, 1)})

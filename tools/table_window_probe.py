@@ -46,7 +46,7 @@ def main():
         torch.cuda.synchronize()
         setup = time.perf_counter() - t0
         line = {"n_bits": 8 * n_bytes, "W": k.table_window, "rows": k.desc.table_rows, "cols": k.desc.table_cols,
-                "key_block_MiB": round(k.block.numel() * 4 / 2**20, 1), "key_setup_ms": round(setup * 1e3, 1)}
+                "key_block_MiB": round(k.block_bytes / 2**20, 1), "key_setup_ms": round(setup * 1e3, 1)}
         for N in a.sizes:
             m = torch.randint(-2**40, 2**40, (N,), dtype=torch.int64, device=dev,
                               generator=torch.Generator(device=dev).manual_seed(N))
@@ -84,7 +84,7 @@ def main():
                 ms = e0.elapsed_time(e1) / 5
                 line[str(N)].update({"crt_ms": round(ms, 3), "crt_encrypts_per_s": round(N / ms * 1e3),
                                      "crt_equal": bool(torch.equal(cc, ct)),
-                                     "crt_tables_MiB": round(sum(sk.block.numel() for sk in subs) * 4 / 2**20, 1)})
+                                     "crt_tables_MiB": round(sum(sk.block_bytes for sk in subs) / 2**20, 1)})
         print(json.dumps(line), flush=True)
         del kp, k
         import gc
