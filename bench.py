@@ -300,6 +300,11 @@ def stage_p(args):
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
     cpu_keys = {}
+    # In production the key owner (sender: CRT sub-tables) and the public-key holder (receiver: the
+    # n^2 table) are different processes, each under its own 4 GiB process-wide table budget. This
+    # report measures both paths of one key in one process, so it gives the process the sum: each
+    # path then runs with the table its own process would build.
+    pc.table_budget(2 * pc.TABLE_MAX_BYTES)
     for label, n_bytes, a_bytes, g, N in STAGE_P_KEYS:
         n, hs, p, q = pc.generate_keypair_ints(n_bytes, 24, random.Random(n_bytes))
         kp = efl.paillier.Keypair(seed=7)
@@ -411,7 +416,9 @@ def stage_p(args):
                                                      out["cpu_baseline"]["encrypt"], 1)
         if "MNIST" in label:
             out["matmul"] = stage_p_matmul(args, efl, pc, kp, lib, sh, stream, dev)
+        out["table_budget"] = dict(zip(("budget", "in_use"), pc.table_budget()))
         print(json.dumps(out), flush=True)
+        k.close()      # the next key's tables are sized against the process-wide budget
 
 
 def stage_p_crt(k, subs, a_bytes, N, t, t_public, t_setup):

@@ -566,6 +566,13 @@ std::atomic<int> g_batch_k[2] = {{2}, {2}};
 std::atomic<int> g_batch_order[2] = {{0}, {0}};
 // efl_fxp_tune 19: workgroups of the persistent batched walk (order 3)
 std::atomic<int> g_batch_persist_grid{2048};
+// The fp64 encode (8 B read, 16 B written per element) through its own shape: efl_fxp_tune kinds
+// 21 workgroup size, 22 units per lane, 23 NT mask, 24 XCD-aware order. Round 4 ran it at the fp32
+// encode's shape (512 lanes, 1 unit, NT 7, linear order): 0.79 of 8 TB/s. Round 5 sweep of all 36
+// shapes, interleaved, median of 3 (tools/fp64_shape_probe.py, profiles/r05/fp64_shape.jsonl):
+// 1024 lanes, 1 unit, NT 7 and the XCD-aware order 0.2508 ms (0.803) against 0.2547 ms (0.790).
+Shape g_shape64 = {{0}, {1024}, {1}, {7}};
+std::atomic<int> g_xcd64{1};
 
 template <class Op, int B, int K, int NT>
 hipError_t launch_k(const typename Op::Args& a, long long nunits, hipStream_t s, int xcd = 0) {
@@ -596,21 +603,20 @@ hipError_t launch_nt(int nt, const typename Op::Args& a, long long nunits, hipSt
 }
 
 template <class Op, int B>
-hipError_t launch_bk(const Shape& sh, const typename Op::Args& a, long long nunits, hipStream_t s) {
+hipError_t launch_bk(const Shape& sh, const typename Op::Args& a, long long nunits, hipStream_t s, int xcd) {
   const int nt = sh.nt.load(std::memory_order_relaxed);
-  const int xcd = g_xcd_order[&sh == &g_shape[kDec] ? kDec : kEnc].load(std::memory_order_relaxed);
   return sh.k.load(std::memory_order_relaxed) == 2 ? launch_nt<Op, B, 2>(nt, a, nunits, s, xcd)
                                                    : launch_nt<Op, B, 1>(nt, a, nunits, s, xcd);
 }
 
-// tunable launch (fp32 ops)
+// tunable launch (fp32 ops; the fp64 encode through its own shape, g_shape64)
 template <class Op>
-hipError_t launch_tuned(const Shape& sh, const typename Op::Args& a, long long nunits, hipStream_t s) {
+hipError_t launch_tuned(const Shape& sh, const typename Op::Args& a, long long nunits, hipStream_t s, int xcd) {
   switch (sh.block.load(std::memory_order_relaxed)) {
-    case 128: return launch_bk<Op, 128>(sh, a, nunits, s);
-    case 512: return launch_bk<Op, 512>(sh, a, nunits, s);
-    case 1024: return launch_bk<Op, 1024>(sh, a, nunits, s);
-    default: return launch_bk<Op, 256>(sh, a, nunits, s);
+    case 128: return launch_bk<Op, 128>(sh, a, nunits, s, xcd);
+    case 512: return launch_bk<Op, 512>(sh, a, nunits, s, xcd);
+    case 1024: return launch_bk<Op, 1024>(sh, a, nunits, s, xcd);
+    default: return launch_bk<Op, 256>(sh, a, nunits, s, xcd);
   }
 }
 
@@ -640,8 +646,13 @@ hipError_t run(int dir, const typename Op::Args& a, const void* p0, const void* 
   const uintptr_t need = 16;
   if (aligned(p0, need) && aligned(p1, need) && aligned(p2, need)) {
     const long long nunits = n / Op::kElems;
-    hipError_t e = TUNED ? launch_tuned<Op>(g_shape[dir], a, nunits, s)
-                         : launch_fixed<Op>(dir, a, nunits, s);
+    hipError_t e;
+    if constexpr (std::is_same<Op, EncF64Pair>::value)
+      e = launch_tuned<Op>(g_shape64, a, nunits, s, g_xcd64.load(std::memory_order_relaxed));
+    else if constexpr (TUNED)
+      e = launch_tuned<Op>(g_shape[dir], a, nunits, s, g_xcd_order[dir].load(std::memory_order_relaxed));
+    else
+      e = launch_fixed<Op>(dir, a, nunits, s);
     if (e != hipSuccess) return e;
     return launch_scalar<Op>(a, nunits * Op::kElems, n, s);
   }
@@ -686,6 +697,22 @@ std::atomic<int> g_dp_blocks{4};
 }  // namespace efl
 
 EFL_API int efl_fxp_tune(int kind, int value) {
+  if (kind >= 21 && kind <= 24) {   // fp64 encode shape
+    switch (kind) {
+      case 21:
+        if (value != 128 && value != 256 && value != 512 && value != 1024) return EFL_E_INVALID_ARGUMENT;
+        return g_shape64.block.exchange(value);
+      case 22:
+        if (value != 1 && value != 2) return EFL_E_INVALID_ARGUMENT;
+        return g_shape64.k.exchange(value);
+      case 23:
+        if (value < 0 || (value > 3 && value != 7)) return EFL_E_INVALID_ARGUMENT;
+        return g_shape64.nt.exchange(value);
+      default:
+        if (value != 0 && value != 1) return EFL_E_INVALID_ARGUMENT;
+        return g_xcd64.exchange(value);
+    }
+  }
   if (kind == 20) {                 // DP noise kernel: Philox blocks per lane (csrc/mask.hip)
     if (value != 1 && value != 2 && value != 4) return EFL_E_INVALID_ARGUMENT;
     return g_dp_blocks.exchange(value);

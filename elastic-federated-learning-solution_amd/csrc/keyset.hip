@@ -620,10 +620,9 @@ struct efl_pl_ctx {
     for (auto& s : sub) t += s ? s->table_bytes : 0;
     return t;
   }
-  int64_t allowance() const {
-    const int64_t c = cap_bytes() - held();
-    return std::max<int64_t>(0, std::min(c, budget_left()));
-  }
+  // the cap bounds each of the context's two table sets (its n^2 table; the key owner's CRT pair),
+  // the process-wide budget bounds them all
+  int64_t allowance() const { return std::max<int64_t>(0, std::min(cap_bytes(), budget_left())); }
   bool crt_enabled() const {
     if (crt_mode >= 0) return crt_mode == 1;
     const char* v = getenv("EFL_PL_CRT_ENCRYPT");
@@ -674,9 +673,10 @@ int ensure_crt(efl_pl_ctx* c, hipStream_t s, bool* ok) {
     c->crt = -1;
     return EFL_OK;
   }
-  // the two sub-tables take 3/8 each of what the context may still hold, so a quarter is left for
-  // the owner's own n^2 table should the public-key path be walked
-  const int64_t each = c->allowance() / 8 * 3;
+  // the two sub-tables take half each of what the context may hold (round 4's split: W = 18 for the
+  // examples' 1024-bit key under the 4 GiB default); the owner's own n^2 table, built only if the
+  // public-key path is walked, is sized against what the budget has left then
+  const int64_t each = c->allowance() / 2;
   std::unique_ptr<Block> sb[2];
   for (int i = 0; i < 2; ++i) {
     const Big& x = i ? m.q : m.p;
@@ -713,7 +713,7 @@ int ensure_table(efl_pl_ctx* c, hipStream_t s) {
   Block& b = *c->main;
   if (b.has_table) return EFL_OK;
   if (!c->window) {
-    // re-plan the window against what is left now (the owner's sub-tables may hold part of it)
+    // re-plan the window against what the budget has left now (the owner's sub-tables hold part)
     const int64_t eb = 4LL * (b.lc + b.L28);
     const int W = choose_window(b.a_bits, eb, c->allowance());
     if (!W) {

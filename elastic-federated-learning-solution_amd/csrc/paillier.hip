@@ -1439,6 +1439,11 @@ EFL_API int efl_pl_tune(int ln, int decrypt, int limbs_per_lane) {
     if (limbs_per_lane > 1) { set_error("decryption method must be 0 (binary) or 1 (window)"); return EFL_E_INVALID_ARGUMENT; }
     return pl::sl_dec_window(limbs_per_lane);
   }
+  if (decrypt == 4) {   // row-split fixed-base walks: 0 chosen per launch, 1 never, 2..5 parts
+    if (limbs_per_lane < 0) return pl::sl_walk_parts(-1);
+    if (limbs_per_lane > 5) { set_error("walk parts must be 0 (auto) or 1..5"); return EFL_E_INVALID_ARGUMENT; }
+    return pl::sl_walk_parts(limbs_per_lane);
+  }
   if (decrypt == 3) {   // efl_pl_matmul term splits: 0 chosen per launch, 1..16 fixed
     if (limbs_per_lane < 0) return pl::sl_mat_splits(-1);
     if (limbs_per_lane > 16) { set_error("matmul term splits must be 0 (auto) or 1..16"); return EFL_E_INVALID_ARGUMENT; }

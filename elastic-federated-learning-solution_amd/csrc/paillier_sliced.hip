@@ -800,6 +800,213 @@ __device__ __forceinline__ void load28(uint32_t (&t)[C28], const uint32_t* __res
   }
 }
 
+// ---- row-split walks (round 5) -------------------------------------------------------------------
+// A launch of W waves keeps every SIMD busy only when W is close to a multiple of the SIMD count:
+// the paillier_mnist activation ([256, 392] = 100,352 elements, 1,568 one-lane waves on 1,024 SIMDs)
+// leaves 480 SIMDs with one wave and 544 with two, so the launch lasts as long as two waves for 1.53
+// waves of work (0.77). Splitting every element's fixed-base walk into P parts over disjoint ranges of
+// table rows (P x the waves, each doing 1/P of the work) evens that out, e.g. 4.59 -> 5 waves per SIMD
+// for P = 3 (0.92). Parts start from their first non-zero window's entry instead of the Montgomery
+// one, so the P - 1 products of the join cost nothing extra; an encryption's join then multiplies
+// the product (x R) by g(m) in normal form, which gives the ciphertext x g with no conversion, two
+// products fewer than k_encrypt28 (g -> g R, and the conversion out). Same value, bit for bit: a
+// product mod m does not depend on its grouping, and every part's lazy result (< 2m) is a valid
+// Montgomery operand.
+
+// the walk over table rows [r0, r1) of a' (regrouped, `size` bits) into acc; `have` = acc already
+// holds a factor (the walk start, or g R); otherwise the first non-zero window's entry becomes acc.
+// Returns whether acc holds a factor afterwards.
+template <int C, int G>
+__device__ __forceinline__ bool walk28_rows(uint32_t (&acc)[s28::limbs_per_lane(C * G, G)], const Key& k, const uint32_t* A,
+                                            uint32_t* B, int E, int words, int size,
+                                            const uint32_t (&m28)[s28::limbs_per_lane(C * G, G)], int g, int r0, int r1,
+                                            bool have) {
+  constexpr int L = C * G;
+  constexpr int C28 = s28::limbs_per_lane(L, G), L28 = C28 * G;
+  const int W = table_window(k.d);
+  const uint32_t minv28 = k.d.n2_minv28;
+  const uint32_t* table = k.at(k.d.off_table28);
+  const int cols = k.d.table_cols;
+  const int end = r1 * W < size ? r1 * W : size;
+  int s = r0 * W, row = r0;
+  auto next_entry = [&]() -> const uint32_t* {
+    for (; s < end; s += W, ++row) {
+      const uint32_t idx = col_bits(A, E, s, end - s < W ? end - s : W, words);
+      if (idx) {
+        const uint32_t* e = walk_entry<C28, L28>(table, row, idx, cols, g);
+        s += W;
+        ++row;
+        return e;
+      }
+    }
+    return nullptr;
+  };
+  const uint32_t* cur = next_entry();
+  if constexpr (G == 1 && EFL_MUL_FIPS) {
+    // as fbpowm28_walk's one-lane loop: the entry goes into registers, the next one is in flight
+    // during the product
+    uint32_t b[C28], nb[C28];
+    if (cur) {
+#pragma unroll
+      for (int j = 0; j < C28; ++j) b[j] = cur[j];
+    }
+    if (!have) {
+      if (!cur) return false;
+#pragma unroll
+      for (int j = 0; j < C28; ++j) acc[j] = b[j];
+      cur = next_entry();
+      if (cur) {
+#pragma unroll
+        for (int j = 0; j < C28; ++j) b[j] = cur[j];
+      }
+    }
+    while (cur) {
+      const uint32_t* nxt = next_entry();
+      if (nxt) {
+#pragma unroll
+        for (int j = 0; j < C28; ++j) nb[j] = nxt[j];
+      }
+      s28::mul_fips1<C28>(acc, b, m28, minv28);
+      cur = nxt;
+#pragma unroll
+      for (int j = 0; j < C28; ++j) b[j] = nb[j];
+    }
+  } else {
+    if (!have) {
+      if (!cur) return false;
+#pragma unroll
+      for (int j = 0; j < C28; ++j) acc[j] = cur[j];
+      cur = next_entry();
+    }
+    while (cur) {
+#pragma unroll
+      for (int j = 0; j < C28; ++j) B[(g * C28 + j) * E] = cur[j];
+      lds_sync();
+      s28::mont_mul<C28, G>(acc, LdsElem{B, E}, m28, minv28, g);
+      lds_sync();
+      cur = next_entry();
+    }
+  }
+  return true;
+}
+
+// part p of element i (virtual element v = p N + i): the product of its rows' entries in radix-2^28
+// Montgomery form into P (padded slices, store28 layout), and whether it holds anything into F.
+// FROM_START (efl_pl_fbpowm): part 0 starts from the key's walk start (off_n2_one28, the CRT
+// sub-keys' R (q^2)^-1); otherwise (PaillierEncrypt) every part starts from its first entry and the
+// join brings in g(m).
+template <int C, int G, bool FROM_START>
+__global__ __launch_bounds__(kSlBlock, C >= 32 ? (G == 1 ? EFL_WALK1_WAVES : 2) : EFL_DEC_WAVES) void k_walk28_part(
+    Key k, const uint32_t* __restrict__ a_in, uint32_t* __restrict__ P, unsigned char* __restrict__ F, long long N,
+    int parts, uint64_t seed, long long ctr0) {
+  constexpr int L = C * G, E = kSlBlock / G;
+  constexpr int C28 = s28::limbs_per_lane(L, G), L28 = C28 * G, CP = pad4<C28>();
+  extern __shared__ uint32_t lds[];
+  SL_ELEMENT(E, G)
+  if (i >= N * parts) return;
+  const long long v = i;
+  const int part = (int)(v / N);
+  const long long el = v - (long long)part * N;
+  const int words = (k.d.a_bits + 31) >> 5;
+  uint32_t* B = lds + e;
+  uint32_t* A = lds + L28 * E + e;
+  uint32_t m28[C28], acc[C28];
+  slice_uniform<C28>(m28, k.at(k.d.off_n2_28), g);
+  bool have = false;
+  if (FROM_START && part == 0) {
+    slice_uniform<C28>(acc, k.at(k.d.off_n2_one28), g);
+    have = true;
+  }
+  if (a_in) {
+    for (int w = g; w < words; w += G) A[w * E] = a_in[el * words + w];
+  } else {
+    draw_a<G>(A, E, words, k.d.a_bits, seed, (uint64_t)(ctr0 + el), g);
+  }
+  lds_sync();
+  const int size = regroup_shared(A, E, words, k.d.group_size, g);
+  const int rows = k.d.table_rows;
+  const int r0 = (int)((long long)rows * part / parts), r1 = (int)((long long)rows * (part + 1) / parts);
+  have = walk28_rows<C, G>(acc, k, A, B, E, words, size, m28, g, r0, r1, have);
+  store28<C28>(P + (size_t)v * G * CP + g * CP, acc);
+  if (g == 0) F[v] = have ? 1 : 0;
+}
+
+// the join: element i's parts multiplied (parts without a factor skipped). m NULL (efl_pl_fbpowm):
+// then out of Montgomery form, as k_fbpowm28 writes it. m given (PaillierEncrypt): the product (x R)
+// times g(m) in normal form is x g, the ciphertext, with one conditional subtraction of n^2 (the
+// walk's lazy bound is 2 n^2) and no conversion; no factor at all (a' = 0) leaves g(m) itself.
+template <int C, int G>
+__global__ __launch_bounds__(kSlBlock, C >= 32 ? (G == 1 ? EFL_WALK1_WAVES : 2) : EFL_DEC_WAVES) void k_walk28_join(
+    Key k, const long long* __restrict__ m, const uint32_t* __restrict__ P, const unsigned char* __restrict__ F,
+    uint32_t* __restrict__ out, long long N, int parts) {
+  constexpr int L = C * G, E = kSlBlock / G;
+  constexpr int C28 = s28::limbs_per_lane(L, G), L28 = C28 * G, CP = pad4<C28>();
+  extern __shared__ uint32_t lds[];
+  SL_ELEMENT(E, G)
+  if (i >= N) return;
+  uint32_t* B = lds + e;
+  uint32_t* GW = lds + L28 * E + e;        // g(m) as 32-bit words, made before the products
+  if (m) {
+    uint32_t c[C], n2[C];
+    slice_uniform<C>(n2, k.at(k.d.off_n2), g);
+    make_g<C, G>(c, m[i], k, n2, g);
+    to_lds<C>(GW, E, g, c);
+    lds_sync();
+  }
+  uint32_t m28[C28], acc[C28];
+  slice_uniform<C28>(m28, k.at(k.d.off_n2_28), g);
+  const uint32_t minv28 = k.d.n2_minv28;
+  bool any = false;
+  for (int p = 0; p < parts; ++p) {
+    const long long v = (long long)p * N + i;
+    if (!F[v]) continue;
+    if (!any) {
+      load28<C28>(acc, P + (size_t)v * G * CP + g * CP);
+      any = true;
+      continue;
+    }
+    uint32_t b[C28];
+    load28<C28>(b, P + (size_t)v * G * CP + g * CP);
+    if constexpr (G == 1 && EFL_MUL_FIPS) {
+      s28::mul_fips1<C28>(acc, b, m28, minv28);
+    } else {
+      to_lds<C28>(B, E, g, b);
+      lds_sync();
+      s28::mont_mul<C28, G>(acc, LdsElem{B, E}, m28, minv28, g);
+      lds_sync();
+    }
+  }
+  if (!m) {
+    store_from_mont28<C, G>(out + i * L, acc, m28, minv28, B, E, g);   // part 0 always holds a factor
+    return;
+  }
+  uint32_t c[C];
+  if (!any) {
+    from_lds<C>(c, GW, E, g);              // a' = 0: the ciphertext is g(m)
+  } else {
+    uint32_t gb[C28];
+    s28::from_words<C28>(gb, GW, E, L, g);
+    lds_sync();
+    if constexpr (G == 1 && EFL_MUL_FIPS) {
+      s28::mul_fips1<C28>(acc, gb, m28, minv28);
+    } else {
+      to_lds<C28>(B, E, g, gb);
+      lds_sync();
+      s28::mont_mul<C28, G>(acc, LdsElem{B, E}, m28, minv28, g);
+      lds_sync();
+    }
+    to_lds<C28>(B, E, g, acc);
+    lds_sync();
+    s28::to_words<C>(c, B, E, L28, g);
+    lds_sync();
+    uint32_t n2[C];
+    slice_uniform<C>(n2, k.at(k.d.off_n2), g);
+    csub<C, G>(c, n2, geq<C, G>(c, n2, g), g);
+  }
+  store_slice<C>(out + i * L, g, c);
+}
+
+
 template <int C, int G>
 __global__ __launch_bounds__(kSlBlock, C >= 32 ? EFL_MAT_WAVES32 : EFL_MAT_WAVES16) void k_matmul28(
     Key k, const uint32_t* __restrict__ Xm, const long long* __restrict__ xe, const long long* __restrict__ ym,
@@ -1339,9 +1546,82 @@ hipError_t run_fbpowm(const Key& k, const uint32_t* a, uint32_t* out, long long 
                      out, N, seed, ctr0);
   return hipGetLastError();
 }
+// SIMDs of the current device (CUs x 4), read once
+int simd_count() {
+  static std::atomic<int> n{0};
+  int v = n.load(std::memory_order_relaxed);
+  if (!v) {
+    int dev = 0, cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cu <= 0)
+      cu = 256;
+    v = 4 * cu;
+    n.store(v, std::memory_order_relaxed);
+  }
+  return v;
+}
+
+// efl_pl_tune(ln, 4, P): parts of the row-split walks, 0 = chosen per launch (walk_parts), 1 = never
+// split, 2..5 = that many whenever the launch is below 4 waves per SIMD
+std::atomic<int> g_walk_parts{0};
+constexpr int kMaxWalkParts = 5;
+
+// Parts for a walk of N elements over G lanes each: the P maximising the share of busy lanes,
+// x P / ceil(x P) for x = waves per SIMD, less about 3 % per extra part (the exponent's draw and
+// regrouping per part, the join's loads); launches of 4 or more waves per SIMD are not split.
+// MNIST activation, 1024-bit key: one-lane CRT walks x = 1.53 -> P = 3 (0.77 -> 0.92 of the lanes
+// busy), the two-lane n^2 walk x = 3.06 -> P = 3 (0.77 -> 0.92).
+int walk_parts(long long N, int G) {
+  const double x = (double)((N * G + 63) / 64) / simd_count();
+  if (x <= 0.0 || x >= 4.0) return 1;
+  const int fixed = g_walk_parts.load(std::memory_order_relaxed);
+  if (fixed > 0) return fixed;
+  int best = 1;
+  double bv = x / __builtin_ceil(x);
+  for (int P = 2; P <= kMaxWalkParts; ++P) {
+    const double u = x * P / __builtin_ceil(x * P) / (1.0 + 0.03 * (P - 1));
+    if (u > bv * 1.02) {
+      best = P;
+      bv = u;
+    }
+  }
+  return best;
+}
+
+// the row-split walk: P parts into stream-ordered scratch, then the join
+template <int C, int G>
+hipError_t run_walk28_split(const Key& k, const long long* m, const uint32_t* a, uint32_t* out, long long N,
+                            uint64_t seed, long long ctr0, int parts, hipStream_t s) {
+  constexpr int L = C * G, E = kSlBlock / G;
+  constexpr int C28 = s28::limbs_per_lane(L, G), L28 = C28 * G;
+  const size_t slot = (size_t)pad4<C28>() * G;
+  const long long V = N * parts;
+  uint32_t* P = nullptr;
+  hipError_t err = hipMallocAsync(reinterpret_cast<void**>(&P), (size_t)V * slot * 4 + (size_t)V, s);
+  if (err != hipSuccess) return err;
+  unsigned char* F = reinterpret_cast<unsigned char*>(P + (size_t)V * slot);
+  const int aw = (k.d.a_bits + 31) / 32;
+  if (m)
+    hipLaunchKernelGGL((k_walk28_part<C, G, false>), dim3(grid_of(V, G)), dim3(kSlBlock), (size_t)(L28 + aw) * E * 4,
+                       s, k, a, P, F, N, parts, seed, ctr0);
+  else
+    hipLaunchKernelGGL((k_walk28_part<C, G, true>), dim3(grid_of(V, G)), dim3(kSlBlock), (size_t)(L28 + aw) * E * 4, s,
+                       k, a, P, F, N, parts, seed, ctr0);
+  err = hipGetLastError();
+  if (err == hipSuccess) {
+    hipLaunchKernelGGL((k_walk28_join<C, G>), dim3(grid_of(N, G)), dim3(kSlBlock), (size_t)2 * L28 * E * 4, s, k, m, P,
+                       F, out, N, parts);
+    err = hipGetLastError();
+  }
+  const hipError_t ferr = hipFreeAsync(P, s);
+  return err != hipSuccess ? err : ferr;
+}
+
 template <int C, int G>
 hipError_t run_encrypt28(const Key& k, const long long* m, uint32_t* out, long long N, uint64_t seed, long long ctr0,
                          hipStream_t s) {
+  const int parts = walk_parts(N, G);
+  if (parts > 1) return run_walk28_split<C, G>(k, m, nullptr, out, N, seed, ctr0, parts, s);
   const int aw = (k.d.a_bits + 31) / 32;
   const size_t lds = (size_t)(s28::limbs_per_lane(C * G, G) * G + aw) * (kSlBlock / G) * 4;
   hipLaunchKernelGGL((k_encrypt28<C, G>), dim3(grid_of(N, G)), dim3(kSlBlock), lds, s, k, m, out, N, seed, ctr0);
@@ -1350,6 +1630,8 @@ hipError_t run_encrypt28(const Key& k, const long long* m, uint32_t* out, long l
 template <int C, int G>
 hipError_t run_fbpowm28(const Key& k, const uint32_t* a, uint32_t* out, long long N, uint64_t seed, long long ctr0,
                         hipStream_t s) {
+  const int parts = walk_parts(N, G);
+  if (parts > 1) return run_walk28_split<C, G>(k, nullptr, a, out, N, seed, ctr0, parts, s);
   const int aw = (k.d.a_bits + 31) / 32;
   const size_t lds = (size_t)(s28::limbs_per_lane(C * G, G) * G + aw) * (kSlBlock / G) * 4;
   hipLaunchKernelGGL((k_fbpowm28<C, G>), dim3(grid_of(N, G)), dim3(kSlBlock), lds, s, k, a, out, N, seed, ctr0);
@@ -1586,6 +1868,9 @@ int sl_dec_window(int v) {
 }
 int sl_mat_splits(int v) {
   return v < 0 ? g_mat_splits.load() : g_mat_splits.exchange(v);
+}
+int sl_walk_parts(int v) {
+  return v < 0 ? g_walk_parts.load() : g_walk_parts.exchange(v);
 }
 hipError_t sl_decrypt(const Key& k, int C, const uint32_t* ct, uint32_t* mag, signed char* neg, long long N,
                       hipStream_t s) {

@@ -192,6 +192,7 @@ int sl_dec_window(int v);
 // efl_pl_matmul's term splits: 0 chosen per launch (default), else 1..16 (rounded down to a power of
 // two); v < 0 queries. Returns the previous setting.
 int sl_mat_splits(int v);
+int sl_walk_parts(int v);
 
 }  // namespace pl
 }  // namespace efl

@@ -116,7 +116,8 @@ _LIMB_CLASSES = (16, 32, 64, 128, 256)
 # PROCESS-WIDE budget shared by every live keypair (table_budget(); EFL_PL_TABLE_BUDGET_MIB, default
 # 4 GiB): a key's window is the widest whose table fits the smaller of its cap and what the budget has
 # left. A public-key holder spends it on its one table; the key owner, whose encryptions go by CRT, on
-# the two CRT sub-tables (3/8 each), building its n^2 table from the rest only if it is ever walked.
+# the two CRT sub-tables (half each), building its n^2 table from what the budget has left only if
+# it is ever walked.
 TABLE_MAX_BYTES = 4 << 30
 WINDOW_MAX = 24
 
@@ -961,33 +962,41 @@ class PaillierKeypair(object):
         = x_ij^y_jk (PaillierMulScalar; x^-1 for y < 0) shifted by 2^(xe_ij + ye_jk - m_ik), m_ik the
         minimum over j, and the terms of an output multiplied mod n^2. Used when the exponents spread
         past MATMUL_MAX_SPREAD: the shifts then run through _exp2_chunked's bounded launches. The
-        product is exact, so the ciphertexts equal efl_pl_matmul's; rows go in chunks of about
-        _COMPOSED_CHUNK_BYTES (256 MiB) of terms."""
+        product is exact, so the ciphertexts equal efl_pl_matmul's. Blocks of rows i and output
+        columns k hold at most about _COMPOSED_CHUNK_BYTES (256 MiB) of terms each (a whole
+        column of v terms at least), so peak memory stays a small multiple of that for any shape."""
         k = self.key
         u, v = x.shape
         w = ym.shape[1]
-        rows = max(1, _COMPOSED_CHUNK_BYTES // (v * w * k.lc * 4))
-        zs, ms = [], []
+        term_bytes = v * k.lc * 4                       # one output's terms
+        wc = max(1, min(w, _COMPOSED_CHUNK_BYTES // term_bytes))
+        rows = max(1, min(u, _COMPOSED_CHUNK_BYTES // (term_bytes * wc)))
+        z = torch.empty((u, w, k.lc), dtype=torch.int32, device=k.device)
+        mins = torch.empty((u, w), dtype=torch.int64, device=k.device)
         for i0 in range(0, u, rows):
             i1 = min(u, i0 + rows)
             r = i1 - i0
             xr = CipherTensor(x.limbs[i0 * v:i1 * v], (r, v, 1), k)
-            t = self.mul_scalar(xr, ym.reshape(1, v, w))                          # [r, v, w]
-            s = xe[i0:i1].reshape(r, v, 1) + ye.reshape(1, v, w)
-            m = s.amin(dim=1)                                                      # [r, w]
-            t = self._exp2_chunked(t.limbs, (s - m.reshape(r, 1, w)).reshape(-1).contiguous())
-            t = t.view(r, v, w, k.lc)
-            while t.shape[1] > 1:                                                  # product over j
-                h = t.shape[1] // 2
-                a = t[:, :h].contiguous()
-                b = t[:, h:2 * h].contiguous()
-                p = torch.empty_like(a)
-                _efl_lib.check(_lib.efl_pl_add(*k.args(), a.data_ptr(), b.data_ptr(), p.data_ptr(),
-                                               r * h * w, _stream(k.device)))
-                t = torch.cat([p, t[:, 2 * h:]], dim=1) if t.shape[1] % 2 else p
-            zs.append(t.reshape(r * w, k.lc))
-            ms.append(m)
-        return CipherTensor(torch.cat(zs).contiguous(), (u, w), k), torch.cat(ms)
+            for k0 in range(0, w, wc):
+                k1 = min(w, k0 + wc)
+                c = k1 - k0
+                yb, yeb = ym[:, k0:k1], ye[:, k0:k1]
+                t = self.mul_scalar(xr, yb.reshape(1, v, c))                      # [r, v, c]
+                s = xe[i0:i1].reshape(r, v, 1) + yeb.reshape(1, v, c)
+                m = s.amin(dim=1)                                                  # [r, c]
+                t = self._exp2_chunked(t.limbs, (s - m.reshape(r, 1, c)).reshape(-1).contiguous())
+                t = t.view(r, v, c, k.lc)
+                while t.shape[1] > 1:                                              # product over j
+                    h = t.shape[1] // 2
+                    a = t[:, :h].contiguous()
+                    b = t[:, h:2 * h].contiguous()
+                    p = torch.empty_like(a)
+                    _efl_lib.check(_lib.efl_pl_add(*k.args(), a.data_ptr(), b.data_ptr(), p.data_ptr(),
+                                                   r * h * c, _stream(k.device)))
+                    t = torch.cat([p, t[:, 2 * h:]], dim=1) if t.shape[1] % 2 else p
+                z[i0:i1, k0:k1] = t.reshape(r, c, k.lc)
+                mins[i0:i1, k0:k1] = m
+        return CipherTensor(z.reshape(u * w, k.lc), (u, w), k), mins
 
     def mul_exp2(self, x, exp):
         """PaillierMulExp2 (paillier.cc:680-751): z = x^(2^y) mod n^2, y int32/int64 >= 0, y

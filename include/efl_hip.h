@@ -77,7 +77,9 @@ const char* efl_last_error(void);
  * kinds 17 / 18 = tile order of the fp32 batched encode / decode (0 2-D grid, 1 one flat tensor-major
  * grid, 2 the flat grid in XCD-aware order, 3 a persistent walk of kind-19 workgroups that loads the
  * next tile while storing the current one); batched workgroup sizes 128, 256, 512; kind 20 =
- * Philox blocks per lane of efl_dp_noise (1, 2, 4; default 4).
+ * Philox blocks per lane of efl_dp_noise (1, 2, 4; default 4); kinds 21-24 = the fp64 encode's
+ * workgroup size (128, 256, 512, 1024), units per lane (1, 2), nontemporal mask (as kind 4) and
+ * XCD-aware tile order (0 / 1).
  * Returns the previous value or EFL_E_INVALID_ARGUMENT. */
 int efl_fxp_tune(int kind, int value);
 
@@ -313,7 +315,11 @@ int efl_pl_matmul(const void* key_block, const efl_pl_key* key, const uint32_t* 
  * caller's stream, up to 2^18 elements x 16 entries per launch), 0 = binary square-and-multiply
  * (no scratch), -1 queries. decrypt = 3 sets efl_pl_matmul's term splits (radix-2^28 family):
  * limbs_per_lane 0 = chosen per launch (default), 1..16 = that many (rounded down to a power of two,
- * at most v), -1 queries. */
+ * at most v), -1 queries. decrypt = 4 sets the row-split fixed-base walks of the radix-2^28 family
+ * (encryption with fresh randomness, efl_pl_fbpowm): a launch of fewer than 4 waves per SIMD splits
+ * every element's walk over 1..5 disjoint ranges of table rows and joins the parts in a second
+ * launch (stream-ordered scratch), so the waves fill the SIMDs; 0 = parts chosen per launch
+ * (default), 1 = never split, 2..5 = that many, -1 queries. Results never change. */
 int efl_pl_tune(int ln, int decrypt, int limbs_per_lane);
 
 /* ---- Key context: the PaillierKeypair resource ----------------------------------------------

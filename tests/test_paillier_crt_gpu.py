@@ -197,7 +197,7 @@ def test_owner_table_deferred_until_walked(efl):
     assert not key.has_table                                   # CRT needs only the sub-tables
     subs = key.crt_keys()
     budget = pc.table_max_bytes()
-    assert all(sk.block_bytes <= budget * 3 // 8 + (1 << 20) for sk in subs)     # 3/8 of the cap each
+    assert all(sk.block_bytes <= budget // 2 + (1 << 20) for sk in subs)     # half of the cap each
     ct = torch.empty((4, key.lc), dtype=torch.int32, device="cuda")
     md = m.cuda()
     rc = pc._lib.efl_pl_encrypt(*key.args(), md.data_ptr(), None, ct.data_ptr(), 4, 21, 5, None)

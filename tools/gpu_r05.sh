@@ -9,7 +9,7 @@ export PYTHONUNBUFFERED=1
 LIBDIR=$PWD/elastic-federated-learning-solution_amd/efl
 run() {
   case "$1" in
-    tests)  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+    tests)  timeout -k 10 1000 python -u -m pytest tests -m gpu -q --maxfail=10 --timeout 300 --timeout-method thread \
               > gpurun_out/r05_pytest.log 2>&1 ;;
     pltests) timeout -k 10 900 python -u -m pytest tests/test_paillier_gpu.py tests/test_paillier_crt_gpu.py \
               tests/test_federal_model_gpu.py tests/test_paillier_reference_cases_gpu.py tests/test_paillier_layer_gpu.py \
@@ -60,6 +60,12 @@ run() {
               EFL_HIP_LIB=$LIBDIR/$lib timeout -k 10 600 python -u bench.py --stage p --no-cpu-baseline \
                 >> gpurun_out/r05_fips_stagep.jsonl 2>> gpurun_out/r05_fips_stagep.err || exit 1
             done ;;
+    fp64)   timeout -k 10 300 python -u tools/fp64_shape_probe.py > gpurun_out/r05_fp64_shape.jsonl 2> gpurun_out/r05_fp64_shape.err ;;
+    ctx)    timeout -k 10 600 python -u -m pytest tests/test_ctx_abi_gpu.py tests/test_paillier_crt_gpu.py -m gpu -x -q \
+              --timeout 300 --timeout-method thread > gpurun_out/r05_ctx.log 2>&1 ;;
+    split)  timeout -k 10 400 python -u tools/walk_split_probe.py > gpurun_out/r05_walk_split.jsonl 2> gpurun_out/r05_walk_split.err ;;
+    splitt) timeout -k 10 600 python -u -m pytest tests/test_walk_split_gpu.py -m gpu -x -q --timeout 300 \
+              --timeout-method thread > gpurun_out/r05_walk_split_tests.log 2>&1 ;;
     *) echo "unknown step $1"; return 2 ;;
   esac
 }
