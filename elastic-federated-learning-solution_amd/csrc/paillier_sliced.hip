@@ -1569,13 +1569,16 @@ constexpr int kMaxWalkParts = 5;
 // Parts for a walk of N elements over G lanes each: the P maximising the share of busy lanes,
 // x P / ceil(x P) for x = waves per SIMD, less about 3 % per extra part (the exponent's draw and
 // regrouping per part, the join's loads); launches of 4 or more waves per SIMD are not split.
-// MNIST activation, 1024-bit key: one-lane CRT walks x = 1.53 -> P = 3 (0.77 -> 0.92 of the lanes
-// busy), the two-lane n^2 walk x = 3.06 -> P = 3 (0.77 -> 0.92).
+// MNIST activation, 1024-bit key: the two-lane n^2 walk x = 3.06 -> P = 3 (0.77 -> 0.92 of the lanes
+// busy): 59.2 -> 77.4 M encryptions/s (profiles/r05/walk_split.jsonl). The one-lane walks (the key
+// owner's CRT sub-keys, G = 1) are not split: their time goes to the table entries' HBM latency,
+// and splitting them measured 1-3 % slower (107.7 -> 104.6 M/s at P = 3).
 int walk_parts(long long N, int G) {
   const double x = (double)((N * G + 63) / 64) / simd_count();
   if (x <= 0.0 || x >= 4.0) return 1;
   const int fixed = g_walk_parts.load(std::memory_order_relaxed);
-  if (fixed > 0) return fixed;
+  if (fixed > 0) return fixed;        // (a fixed P splits the one-lane walks too: A/B, tests)
+  if (G == 1) return 1;
   int best = 1;
   double bv = x / __builtin_ceil(x);
   for (int P = 2; P <= kMaxWalkParts; ++P) {

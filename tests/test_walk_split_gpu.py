@@ -84,8 +84,8 @@ def test_every_split_gives_the_unsplit_walk(efl, k):
 
 def test_mnist_shape_split_round_trip(efl):
     """The paillier_mnist activation ([256, 392], 100,352 mantissas), 1024-bit key: the split chosen
-    per launch (P = 3 on 256 CUs) for the key owner's CRT walks and for the public-key holder's n^2
-    walk give the unsplit ciphertexts, which decrypt to the plaintext."""
+    per launch (P = 3 on 256 CUs for the public-key holder's two-lane n^2 walk; the key owner's
+    one-lane CRT walks stay whole) gives the unsplit ciphertexts, which decrypt to the plaintext."""
     k = next(k for k in KAT["keys"] if k["n_bytes"] == 128)
     ln = 32
     g = torch.Generator(device="cuda").manual_seed(5)

@@ -66,6 +66,15 @@ run() {
     split)  timeout -k 10 400 python -u tools/walk_split_probe.py > gpurun_out/r05_walk_split.jsonl 2> gpurun_out/r05_walk_split.err ;;
     splitt) timeout -k 10 600 python -u -m pytest tests/test_walk_split_gpu.py -m gpu -x -q --timeout 300 \
               --timeout-method thread > gpurun_out/r05_walk_split_tests.log 2>&1 ;;
+    crtkt)  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r05_crtkt -o run --output-format csv \
+              -- python3 tools/crt_mnist_probe.py --parts 1 > gpurun_out/r05_crtkt.log 2>&1 ;;
+    profp)  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/r05_prof_p -o run --output-format csv \
+              -- python3 bench.py --stage p --no-cpu-baseline > gpurun_out/r05_prof_p.log 2>&1 ;;
+    spillkt) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r05_spill_kt -o run --output-format csv \
+              -- python3 tools/spill_probe.py > gpurun_out/r05_spill_kt.log 2>&1 ;;
+    spillpmc) timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_FLAT SQ_ACTIVE_INST_FLAT SQ_WAVE_CYCLES SQ_INSTS \
+              -d gpurun_out/r05_spill_pmc -o run --output-format csv \
+              -- python3 tools/spill_probe.py > gpurun_out/r05_spill_pmc.log 2>&1 ;;
     *) echo "unknown step $1"; return 2 ;;
   esac
 }
