@@ -24,6 +24,7 @@
 
 #include "common.h"
 #include "hostbig.h"
+#include "pl_common.h"
 
 using efl::hb::Big;
 namespace hb = efl::hb;
@@ -388,6 +389,7 @@ int plan_block(Block& b, const Big& n, const Big& hs, int a_bits, int g, const B
   d.table_cols = cols;
   d.table_window = W;
   d.off_table28 = -1;
+  d.off_gn28 = d.off_gstart28 = -1;
   d.off_table = -1;
   d.table_rows = 0;                 // no table attached yet: the walks refuse (table_ok)
   if (fam > 0) {
@@ -689,6 +691,17 @@ int ensure_crt(efl_pl_ctx* c, hipStream_t s, bool* ok) {
       return EFL_OK;
     }
     if (rc != EFL_OK) return rc;
+    if (sb[i]->L28) {
+      // the per-element walk start (y^2)^-1 g(m) mod x^2 (efl_pl_key off_gn28 / off_gstart28)
+      Block& b = *sb[i];
+      const Big& y2 = i ? p2 : q2;
+      Big y2inv;
+      if (hb::modinv(y2, x2, &y2inv)) {
+        const Big R28 = hb::pow2(28 * b.L28);
+        b.d.off_gn28 = put28(b.head, hb::mod(hb::shl(hb::mod(m.n, x2), 84), x2), b.L28);
+        b.d.off_gstart28 = put28(b.head, hb::mod(hb::mul(y2inv, hb::mod(hb::mul(R28, R28), x2)), x2), b.L28);
+      }
+    }
     if (c->window && planned_table_bytes(*sb[i]) > budget_left()) {
       c->crt = -1;
       return EFL_OK;
@@ -1009,10 +1022,21 @@ static int crt_run(efl_pl_ctx* c, const uint32_t* a, const int64_t* m, uint32_t*
   const Block& mb = *c->main;
   Scratch sc(s);
   uint32_t* y[2] = {nullptr, nullptr};
-  for (int i = 0; i < 2; ++i) {
-    KS_HIP(sc.get((void**)&y[i], (size_t)n * c->sub[i]->lc * 4), "CRT scratch");
-    KS_RC(efl_pl_fbpowm(c->sub[i]->dev, &c->sub[i]->d, a, y[i], n, seed, ctr, s));
+  for (int i = 0; i < 2; ++i) KS_HIP(sc.get((void**)&y[i], (size_t)n * c->sub[i]->lc * 4), "CRT scratch");
+  // round 5: each walk starts from the element's (y^2)^-1 g(m), so the join of the two walks is the
+  // ciphertext and no product mod n^2 is left (k_fbpowm28g); otherwise the walks start from the
+  // key's R (y^2)^-1 and the join multiplies by g(m) mod n^2 (efl_pl_crt_join with the plaintext)
+  bool direct = c->sub[0]->d.off_gn28 >= 0 && c->sub[1]->d.off_gn28 >= 0;
+  for (int i = 0; i < 2 && direct; ++i) {
+    const Block& sb = *c->sub[i];
+    const int fam = efl_pl_tune(sb.ln, 0, -1);
+    const hipError_t e = pl::sl_fbpowm_g(pl::Key{sb.dev, sb.d}, fam > 0 ? fam : 0, (const long long*)m, a, y[i],
+                                         (long long)n, seed, (long long)ctr, s);
+    if (e == hipErrorNotSupported) direct = false;
+    else if (e != hipSuccess) return hip_fail(e, "CRT walk");
   }
+  if (direct) return efl_pl_crt_join(mb.dev, &mb.d, y[0], y[1], nullptr, out, n, s);
+  for (int i = 0; i < 2; ++i) KS_RC(efl_pl_fbpowm(c->sub[i]->dev, &c->sub[i]->d, a, y[i], n, seed, ctr, s));
   const int64_t* mm = m;
   if (!mm) {                         // g(0) = 1: the join gives hs^(a') itself
     int64_t* z = nullptr;

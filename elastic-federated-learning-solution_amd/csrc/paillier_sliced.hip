@@ -318,12 +318,18 @@ __device__ __forceinline__ void fbpowm28_walk(uint32_t (&acc)[s28::limbs_per_lan
 // hs^(a') mod n^2 through the radix-2^28 table (gmp_utils.cc:107-144), as 32-bit words
 template <int C, int G>
 __device__ __forceinline__ void fbpowm28(uint32_t (&out)[C], const Key& k, uint32_t* A, uint32_t* B, int E,
-                                         int words, int g) {
+                                         int words, int g, const uint32_t* start = nullptr) {
   constexpr int L = C * G;
   constexpr int C28 = s28::limbs_per_lane(L, G), L28 = C28 * G;
   uint32_t m28[C28], acc[C28];
   slice_uniform<C28>(m28, k.at(k.d.off_n2_28), g);
-  slice_uniform<C28>(acc, k.at(k.d.off_n2_one28), g);
+  if (start) {                                    // the element's own walk start (k_gstart28)
+    constexpr int CP = (C28 + 3) & ~3;
+#pragma unroll
+    for (int j = 0; j < C28; ++j) acc[j] = start[g * CP + j];
+  } else {
+    slice_uniform<C28>(acc, k.at(k.d.off_n2_one28), g);
+  }
   fbpowm28_walk<C, G>(acc, k, A, B, E, words, m28, g);
   s28::mont_mul<C28, G>(acc, Unit{}, m28, k.d.n2_minv28, g);   // hs^(a') mod n^2 (< n^2)
   lds_sync();
@@ -336,7 +342,8 @@ __device__ __forceinline__ void fbpowm28(uint32_t (&out)[C], const Key& k, uint3
 template <int C, int G>
 __global__ __launch_bounds__(kSlBlock, C >= 32 ? (G == 1 ? EFL_WALK1_WAVES : 2) : EFL_DEC_WAVES) void k_fbpowm28(Key k, const uint32_t* __restrict__ a_in,
                                                                          uint32_t* __restrict__ out, long long N,
-                                                                         uint64_t seed, long long ctr0) {
+                                                                         uint64_t seed, long long ctr0,
+                                                                         const uint32_t* __restrict__ start) {
   constexpr int L = C * G, E = kSlBlock / G;
   constexpr int L28 = s28::limbs_per_lane(L, G) * G;
   extern __shared__ uint32_t lds[];
@@ -352,8 +359,62 @@ __global__ __launch_bounds__(kSlBlock, C >= 32 ? (G == 1 ? EFL_WALK1_WAVES : 2) 
   }
   lds_sync();
   uint32_t h[C];
-  fbpowm28<C, G>(h, k, A, B, E, words, g);
+  fbpowm28<C, G>(h, k, A, B, E, words, g, start ? start + (size_t)i * G * ((s28::limbs_per_lane(L, G) + 3) & ~3) : nullptr);
   store_slice<C>(out + i * L, g, h);
+}
+
+// |m|'s 28-bit limbs as a b operand (three steps cover |m| < 2^84)
+struct MLimbs {
+  unsigned long long v;
+  __device__ __forceinline__ uint32_t operator()(int i) const {
+    return i < 3 ? (uint32_t)(v >> (28 * i)) & s28::kMask : 0u;
+  }
+};
+
+// The key owner's CRT walk mod x^2 (x = p or q, y the other prime) started from the element's own
+// (y^2)^-1 g(m) instead of the key's fixed walk start: the walk (k_fbpowm28 with `start`) then gives
+// (y^2)^-1 g(m) hs^(a') mod x^2, so the CRT join of the two walks (efl_pl_crt_join without a
+// plaintext: q^2 yp + p^2 yq mod n^2) IS the ciphertext g(m) hs^(a') mod n^2 (paillier.cc:103-131),
+// with no product mod n^2 left. This kernel makes the starts, in the walk's radix-2^28 Montgomery
+// form, into scratch (a separate launch keeps the walk's registers as they are):
+// g(m) mod x^2 = 1 + |m| n, or (1 + |m| n)^-1 = 1 - |m| n for m < 0 (n^2 = 0 mod x^2); |m| (n mod
+// x^2) by three Montgomery steps against (n mod x^2) 2^84 (key constant off_gn28), one conditional
+// subtraction, then one product by (y^2)^-1 R28^2 (off_gstart28) gives (y^2)^-1 g R28. About 1.1
+// products per walk against the 32-bit product mod n^2 it replaces. m NULL: g = 1 (FixedBasePowm).
+template <int C, int G>
+__global__ __launch_bounds__(kSlBlock, C >= 32 ? (G == 1 ? EFL_WALK1_WAVES : 2) : EFL_DEC_WAVES) void k_gstart28(
+    Key k, const long long* __restrict__ m, uint32_t* __restrict__ start, long long N) {
+  constexpr int L = C * G, E = kSlBlock / G;
+  constexpr int C28 = s28::limbs_per_lane(L, G), L28 = C28 * G;
+  extern __shared__ uint32_t lds[];
+  SL_ELEMENT(E, G)
+  if (i >= N) return;
+  uint32_t* B = lds + e;
+  const uint32_t minv28 = k.d.n2_minv28;
+  uint32_t m28[C28], acc[C28];
+  slice_uniform<C28>(m28, k.at(k.d.off_n2_28), g);
+  const long long mi = m ? m[i] : 0;
+  const unsigned long long am = mi < 0 ? 0ull - (unsigned long long)mi : (unsigned long long)mi;
+  slice_uniform<C28>(acc, k.at(k.d.off_gn28), g);
+  s28::mont_mul_steps<C28, G>(acc, MLimbs{am}, m28, minv28, g, 3);         // |m| (n mod x^2), < x^2 (1 + 2^-21)
+  to_lds<C28>(B, E, g, acc);
+  lds_sync();
+  {
+    uint32_t t[C], x2[C];
+    s28::to_words<C>(t, B, E, L28, g);
+    lds_sync();
+    slice_uniform<C>(x2, k.at(k.d.off_n2), g);
+    csub<C, G>(t, x2, geq<C, G>(t, x2, g), g);                              // < x^2
+    if (mi < 0) rsub<C, G>(t, x2, g);                                        // x^2 - t
+    add_small<C, G>(t, 1u, g);                                               // g(m) mod x^2 (<= x^2)
+    to_lds<C>(B, E, g, t);
+    lds_sync();
+  }
+  s28::from_words<C28>(acc, B, E, L, g);
+  s28::mont_mul<C28, G>(acc, Uniform{k.at(k.d.off_gstart28)}, m28, minv28, g);   // (y^2)^-1 g R28
+  constexpr int CP = (C28 + 3) & ~3;            // padded slices, as k_fbpowm28 reads them
+#pragma unroll
+  for (int j = 0; j < C28; ++j) start[(size_t)i * G * CP + g * CP + j] = acc[j];
 }
 
 template <int C, int G>
@@ -1637,8 +1698,28 @@ hipError_t run_fbpowm28(const Key& k, const uint32_t* a, uint32_t* out, long lon
   if (parts > 1) return run_walk28_split<C, G>(k, nullptr, a, out, N, seed, ctr0, parts, s);
   const int aw = (k.d.a_bits + 31) / 32;
   const size_t lds = (size_t)(s28::limbs_per_lane(C * G, G) * G + aw) * (kSlBlock / G) * 4;
-  hipLaunchKernelGGL((k_fbpowm28<C, G>), dim3(grid_of(N, G)), dim3(kSlBlock), lds, s, k, a, out, N, seed, ctr0);
+  hipLaunchKernelGGL((k_fbpowm28<C, G>), dim3(grid_of(N, G)), dim3(kSlBlock), lds, s, k, a, out, N, seed, ctr0,
+                     (const uint32_t*)nullptr);
   return hipGetLastError();
+}
+template <int C, int G>
+hipError_t run_fbpowm28g(const Key& k, const long long* m, const uint32_t* a, uint32_t* out, long long N,
+                         uint64_t seed, long long ctr0, hipStream_t s) {
+  constexpr int C28 = s28::limbs_per_lane(C * G, G), L28 = C28 * G;
+  const int aw = (k.d.a_bits + 31) / 32;
+  uint32_t* st = nullptr;
+  hipError_t err = hipMallocAsync(reinterpret_cast<void**>(&st), (size_t)N * G * ((C28 + 3) & ~3) * 4, s);
+  if (err != hipSuccess) return err;
+  const size_t lds0 = (size_t)(L28 > C * G ? L28 : C * G) * (kSlBlock / G) * 4;
+  hipLaunchKernelGGL((k_gstart28<C, G>), dim3(grid_of(N, G)), dim3(kSlBlock), lds0, s, k, m, st, N);
+  err = hipGetLastError();
+  if (err == hipSuccess) {
+    const size_t lds = (size_t)(L28 + aw) * (kSlBlock / G) * 4;
+    hipLaunchKernelGGL((k_fbpowm28<C, G>), dim3(grid_of(N, G)), dim3(kSlBlock), lds, s, k, a, out, N, seed, ctr0, st);
+    err = hipGetLastError();
+  }
+  const hipError_t ferr = hipFreeAsync(st, s);
+  return err != hipSuccess ? err : ferr;
 }
 template <int C, int G, class XS>
 hipError_t run_powm28(const Key& k, const uint32_t* x, XS xs, uint32_t* out, long long N, unsigned long long* bad,
@@ -1824,6 +1905,11 @@ hipError_t sl_fbpowm(const Key& k, int C, const uint32_t* a, uint32_t* out, long
     SL_DISPATCH(2 * k.d.ln, C, (run_fbpowm28<CC, GG>(k, a, out, N, seed, ctr0, s)))
   }
   SL_DISPATCH(2 * k.d.ln, C, (run_fbpowm<CC, GG>(k, a, out, N, seed, ctr0, s)))
+}
+hipError_t sl_fbpowm_g(const Key& k, int C, const long long* m, const uint32_t* a, uint32_t* out, long long N,
+                       uint64_t seed, long long ctr0, hipStream_t s) {
+  if (!C || !table28_for(k, C) || k.d.off_gn28 < 0 || k.d.off_gstart28 < 0) return hipErrorNotSupported;
+  SL_DISPATCH(2 * k.d.ln, C, (run_fbpowm28g<CC, GG>(k, m, a, out, N, seed, ctr0, s)))
 }
 hipError_t sl_add(const Key& k, int C, const uint32_t* x, const uint32_t* y, uint32_t* out, long long N,
                   hipStream_t s) {

@@ -165,6 +165,11 @@ hipError_t sl_encrypt(const Key& k, int C, const long long* m, const uint32_t* h
                       uint64_t seed, long long ctr0, hipStream_t s, int hsa_mont = 0);
 hipError_t sl_fbpowm(const Key& k, int C, const uint32_t* a, uint32_t* out, long long N, uint64_t seed,
                      long long ctr0, hipStream_t s);
+// the key owner's CRT walk from the element's own start (y^2)^-1 g(m) mod x^2 (k_fbpowm28g; the
+// sub-key's off_gn28 / off_gstart28): hipErrorNotSupported when the sub-key has no such constants or
+// its radix-2^28 table does not serve family C
+hipError_t sl_fbpowm_g(const Key& k, int C, const long long* m, const uint32_t* a, uint32_t* out, long long N,
+                       uint64_t seed, long long ctr0, hipStream_t s);
 hipError_t sl_add(const Key& k, int C, const uint32_t* x, const uint32_t* y, uint32_t* out, long long N,
                   hipStream_t s);
 hipError_t sl_powm(const Key& k, int C, const uint32_t* x, const uint32_t* e, int ew, uint32_t* out, long long N,

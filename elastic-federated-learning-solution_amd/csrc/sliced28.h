@@ -136,6 +136,32 @@ __device__ __forceinline__ void mont_mul(uint32_t (&a)[C], const B& b, const uin
   normalize<C, G>(a, T, g);
 }
 
+// a <- a b 2^(-28 steps) mod m for a b operand of only `steps` limbs (the rest zero): the first
+// `steps` CIOS steps of mont_mul. Inputs a < 2m, b < 2^(28 steps): output < a b 2^(-28 steps) + m.
+template <int C, int G, class B>
+__device__ __forceinline__ void mont_mul_steps(uint32_t (&a)[C], const B& b, const uint32_t (&m)[C], uint32_t minv,
+                                               int g, int steps) {
+  uint64_t T[C];
+#pragma unroll
+  for (int j = 0; j < C; ++j) T[j] = 0;
+  for (int i = 0; i < steps; ++i) {
+    const uint32_t bi = b(i);
+#pragma unroll
+    for (int j = 0; j < C; ++j) T[j] = (uint64_t)a[j] * bi + T[j];
+    const uint32_t u = sl::bcast0<G>(((uint32_t)T[0] * minv) & kMask);
+#pragma unroll
+    for (int j = 0; j < C; ++j) T[j] = (uint64_t)m[j] * u + T[j];
+    uint64_t in = from_next64<G>(T[0]);
+    if (g == G - 1) in = 0;
+    const uint64_t c0 = T[0] >> kBits;
+#pragma unroll
+    for (int j = 0; j < C - 1; ++j) T[j] = T[j + 1];
+    T[C - 1] = in;
+    if (g == 0) T[0] += c0;
+  }
+  normalize<C, G>(a, T, g);
+}
+
 // a <- a^2 R^-1 mod m for a number held in ONE lane (G = 1: the 1024-bit key's decryption family,
 // n^2 of 512-bit keys): finely integrated product scanning (Koc, Acar, Kaliski 1996, "FIPS").
 // Column k of the square takes every cross product a_i a_j (i < j) once and doubles the column, and

@@ -46,7 +46,8 @@ class PlKey(ctypes.Structure):
                 ("off_p2_r2_28", ctypes.c_int64 * 6), ("off_q2_r2_28", ctypes.c_int64 * 6),
                 ("n2_28_len", ctypes.c_int32), ("table28_log2g", ctypes.c_int32), ("n2_minv28", ctypes.c_uint32),
                 ("off_n2_28", ctypes.c_int64), ("off_n2_one28", ctypes.c_int64), ("off_table28", ctypes.c_int64),
-                ("off_n2_r2_28", ctypes.c_int64), ("table_window", ctypes.c_int32)]
+                ("off_n2_r2_28", ctypes.c_int64), ("table_window", ctypes.c_int32),
+                ("off_gn28", ctypes.c_int64), ("off_gstart28", ctypes.c_int64)]
 
 
 _PK = ctypes.POINTER(PlKey)

@@ -197,6 +197,13 @@ typedef struct {
    * plain W-bit windows, so W is the build's choice and does not change any result; 0 = W is
    * group_size (the reference's own table, gmp_utils.cc:56-89). */
   int32_t table_window;
+  /* The key owner's CRT sub-keys only (key (x, hs mod x^2) for x = p or q, y the other prime; -1
+   * elsewhere): radix-2^28 constants (n2_28_len limbs) with which the walk starts from
+   * (y^2)^-1 g(m) mod x^2 for each element's plaintext m, so the CRT join of the two walks is the
+   * ciphertext itself (efl_pl_ctx_encrypt; the g(m) product mod n^2 then disappears):
+   *   off_gn28      (n mod x^2) 2^84 mod x^2: |m| (n mod x^2) by three Montgomery steps
+   *   off_gstart28  (y^2)^-1 R28^2 mod x^2, R28 = 2^(28 n2_28_len): g R28 (y^2)^-1 by one product */
+  int64_t off_gn28, off_gstart28;
 } efl_pl_key;
 
 /*
