@@ -340,14 +340,12 @@ def stage_p(args):
         t_crt = time.perf_counter() - t_crt
         fns = [("encrypt", enc), ("decrypt", dec)]
         if subs:
-            xs = [torch.empty((N, sk.lc), dtype=torch.int32, device=dev) for sk in subs]
             ct_crt = torch.empty_like(ct)
 
             def enc_crt():
-                for sk, x in zip(subs, xs):
-                    efl.lib.check(lib.efl_pl_fbpowm(*sk.args(), None, x.data_ptr(), N, 7, 0, sh))
-                efl.lib.check(lib.efl_pl_crt_join(*k.args(), xs[0].data_ptr(), xs[1].data_ptr(), m.data_ptr(),
-                                                  ct_crt.data_ptr(), N, sh))
+                # the key context's route for the owner (efl_pl_ctx_encrypt): both walks start from
+                # each element's (y^2)^-1 g(m) and the CRT join is the ciphertext (round 5)
+                efl.lib.check(lib.efl_pl_ctx_encrypt(k.ctx, m.data_ptr(), None, ct_crt.data_ptr(), N, 7, 0, 0, sh))
             fns.append(("encrypt_crt", enc_crt))
         times = {}
         for name, fn in fns:
@@ -422,17 +420,19 @@ def stage_p(args):
 
 
 def stage_p_crt(k, subs, a_bytes, N, t, t_public, t_setup):
-    """The key owner's encryption by CRT: algorithmic limb MACs = the two half-length fixed-base
-    walks (one product per non-zero window of each sub-table) + the join (the plain products q^2 yp
-    and p^2 yq) + one product mod n^2 (g(m) times the join's hsa R)."""
+    """The key owner's encryption by CRT (efl_pl_ctx_encrypt): algorithmic limb MACs = the two
+    half-length fixed-base walks (one product per non-zero window of each sub-table), each walk's
+    start (y^2)^-1 g(m) (one product mod x^2, plus three Montgomery steps for |m| (n mod x^2)) and the
+    join (the plain products q^2 yp and p^2 yq). Round 4's route multiplied g(m) into the join's
+    hsa R by one product mod n^2 instead of the two start products."""
     macs = sum(_mont_macs(sk.lc, 0, -(-8 * a_bytes // sk.table_window) * (1 - 2.0 ** -sk.table_window))
-               for sk in subs) + 2 * k.ln * k.ln + _mont_macs(k.lc, 0, 1)
+               + _mont_macs(sk.lc, 0, 1) + 3 * 2 * sk.lc for sk in subs) + 2 * k.ln * k.ln
     issued = sum(_mont_macs(sk.desc.n2_28_len if sk.desc.off_table28 >= 0 else sk.lc, 0,
                             -(-8 * a_bytes // sk.table_window) * (1 - 2.0 ** -sk.table_window)) for sk in subs)
     per_s = N / t
     return {"elements_per_s": round(per_s), "ms": round(t * 1e3, 3), "vs_public_path": round(t_public / t, 3),
             "macs_per_element": int(macs),
-            "method": "hs^a' R mod p^2 and mod q^2 (W=%d/%d), CRT join, mont(g(m), hsa R) mod n^2"
+            "method": "(y^2)^-1 g(m) hs^a' mod p^2 and mod q^2 (W=%d/%d), CRT join = the ciphertext"
                       % (subs[0].table_window, subs[1].table_window),
             "roofline": {"bound": "valu", "achieved": round(per_s * macs / 1e12, 3),
                          "peak": round(MAD_U64_U32_PEAK / 1e12, 3), "unit": "TMAC/s",

@@ -213,6 +213,31 @@ def test_f64_and_int_vs_oracle(efl, n):
         assert np.array_equal(host(fp.mantissa), xi.astype(np.int64))
 
 
+@pytest.mark.parametrize("knob", [(21, 256), (21, 512), (21, 1024), (22, 2), (23, 1), (23, 3), (24, 0), (24, 1)])
+def test_f64_encode_shapes_identical(efl, knob):
+    """Every launch shape of the fp64 encode (efl_fxp_tune 21-24: workgroup size, units per lane,
+    NT mask, XCD-aware order) gives the oracle's bits, ragged tails and tiles smaller than a grid
+    included (fixed_point.cc:144-192)."""
+    lib = efl.lib.raw()
+    n = (1 << 20) + 13
+    rng = np.random.default_rng(knob[0] * 1000 + knob[1])
+    xb = rng.integers(0, 1 << 63, n, dtype=np.uint64) | (rng.integers(0, 2, n, dtype=np.uint64) << np.uint64(63))
+    xd = xb.view(np.float64)
+    Mo, Eo = fxp.encode(xd)
+    prev = lib.efl_fxp_tune(*knob)
+    assert prev >= 0
+    try:
+        for dp in (False, True):
+            fp = efl.paillier.fixedpoint.encode(dev(xd), decrease_precision=dp)
+            if not dp:
+                assert np.array_equal(host(fp.mantissa), Mo) and np.array_equal(host(fp.exponent), Eo)
+            else:
+                Md, Ed = fxp.encode(xd, decrease_precision=True)
+                assert np.array_equal(host(fp.mantissa), Md) and np.array_equal(host(fp.exponent), Ed)
+    finally:
+        lib.efl_fxp_tune(knob[0], prev)
+
+
 @pytest.mark.parametrize("offset", [1, 2, 3])
 def test_unaligned_views(efl, offset):
     n = 10007

@@ -97,3 +97,16 @@ def test_host_sqr_chain_matches_repeated_powers():
     from efl import errors
     with pytest.raises(errors.InvalidArgumentError):
         pc.host_sqr_chain(5, 1, 2, 10, 1)
+
+
+def test_keys_below_128_bits_refused_before_the_prime_search():
+    """n_bytes < 16 (primes of 16..60 bits): the device kernels need n of 128 bits or more, and the
+    sieve would discard every prime of 16 bits or fewer, so the search is refused at once
+     instead of looping."""
+    import time
+    from efl import errors
+    t0 = time.perf_counter()
+    for nb in (1, 2, 4, 8, 15):
+        with pytest.raises(errors.UnimplementedError, match="128 bits"):
+            pc.generate_keypair_ints(nb, 4, random.Random(nb))
+    assert time.perf_counter() - t0 < 1.0

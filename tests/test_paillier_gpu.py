@@ -580,3 +580,22 @@ def test_fixed_point_matmul_and_mul_like_reference_test(efl):
     c3.mantissa = c3.mantissa.decrypt()
     c3 = efl.paillier.fixedpoint.decode(c3)
     assert torch.allclose(a @ bm, c3, 1e-5, 1e-4)
+
+
+def test_refused_rekey_keeps_the_old_key(efl):
+    """A re-key the library refuses on the host (an even n, a_bytes out of range, n past 8192 bits)
+    leaves the keypair's previous key working (the old key used to be dropped first)."""
+    from efl import errors
+    k = ENC_KEYS[1]
+    kp = keypair(efl, k)
+    vs = k["vectors"][:4]
+    hsa = [v["hsa"] for v in vs]
+    m = torch.tensor([v["m"] for v in vs], dtype=torch.int64)
+    before = kp.key
+    for bad in (dict(n=int(k["n"], 16) + 1, a=64), dict(n=int(k["n"], 16), a=0), dict(n=(1 << 8200) + 1, a=64)):
+        with pytest.raises((errors.InvalidArgumentError, errors.UnimplementedError)):
+            kp.set_keys_ints(bad["n"], int(k["hs"], 16), bad["a"], 1)
+        assert kp.key is before
+        assert kp.encrypt(m, hsa=hsa).tensor.to_hex().strings() == [v["c"] for v in vs]
+        assert kp.decrypt(efl.HexTensor.from_strings([v["c"] for v in vs]), dtype=torch.int64).cpu().tolist() == \
+            [v["m"] for v in vs]
