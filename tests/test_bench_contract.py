@@ -1,5 +1,5 @@
 """The BENCH line's contract (the driver parses bench.py's one JSON line), checked on the line the
-final round-4 build printed on the MI355X box (profiles/r04/bench.json) and on the code that makes
+final round-5 build printed on the MI355X box (profiles/r05/bench.json) and on the code that makes
 it: every required key, the roofline and cpu_baseline objects, and their internal consistency."""
 import json
 import os
@@ -11,7 +11,7 @@ REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step
 
 
 def _line():
-    with open(os.path.join(ROOT, "profiles", "r04", "bench.json")) as f:
+    with open(os.path.join(ROOT, "profiles", "r05", "bench.json")) as f:
         lines = [ln for ln in f.read().splitlines() if ln.startswith("{")]
     assert len(lines) == 1
     return json.loads(lines[0])
@@ -46,6 +46,15 @@ def test_cpu_baseline_object():
     assert c["kind"] in ("port", "reference") and c["cores"] >= 1 and c["unit"] == "GiB/s"
 
 
+def test_rank_devices_reported():
+    """Every rank's observed device: devices_used is the distinct count of what
+    the ranks reported."""
+    d = _line()
+    rd = d["rank_devices"]
+    assert len(rd) == d["n_gpus"] and all(r["pci"] for r in rd)
+    assert d["devices_used"] == len({(r["host"], r["pci"]) for r in rd})
+
+
 def test_config3_both_layouts_reported():
     c3 = _line()["config3"]
     assert c3["roundtrip_ok"] and c3["views"]["roundtrip_ok"]
@@ -77,7 +86,7 @@ def test_records_come_from_the_shipping_library():
     and the Stage P report carries the GMP CPU baseline of the same run (bench hygiene)."""
     h = _src_hash()
     assert _line()["library"].endswith("src " + h)
-    with open(os.path.join(ROOT, "profiles", "r04", "bench_stage_p.jsonl")) as f:
+    with open(os.path.join(ROOT, "profiles", "r05", "bench_stage_p.jsonl")) as f:
         lines = [json.loads(ln) for ln in f if ln.startswith("{")]
     assert len(lines) == 3
     for d in lines:

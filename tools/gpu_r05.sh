@@ -68,6 +68,10 @@ run() {
               --timeout-method thread > gpurun_out/r05_walk_split_tests.log 2>&1 ;;
     crtkt)  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r05_crtkt -o run --output-format csv \
               -- python3 tools/crt_mnist_probe.py --parts 1 > gpurun_out/r05_crtkt.log 2>&1 ;;
+    crtkt3) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r05_crtkt3 -o run --output-format csv \
+              -- python3 tools/crt_mnist_probe.py --parts 3 > gpurun_out/r05_crtkt3.log 2>&1 ;;
+    crtkt2) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r05_crtkt2 -o run --output-format csv \
+              -- python3 tools/crt_mnist_probe.py --n 262144 > gpurun_out/r05_crtkt2.log 2>&1 ;;
     profp)  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/r05_prof_p -o run --output-format csv \
               -- python3 bench.py --stage p --no-cpu-baseline > gpurun_out/r05_prof_p.log 2>&1 ;;
     spillkt) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r05_spill_kt -o run --output-format csv \
