@@ -23,6 +23,7 @@
 
 #include "common.h"
 #include "pl_common.h"
+#include "box_muller_math.h"
 #include "sincos_angle.h"
 
 // Every product and sum rounds on its own, as TF's separate ops (and numpy in the oracle) do:
@@ -215,11 +216,14 @@ __global__ __launch_bounds__(kBlock) void k_mask_rows(const float* __restrict__ 
 // (0, 1) and (2, 3): u1 = max(Uint32ToFloat(x0), 1e-7), v1 = float(2 pi (double) * Uint32ToFloat(x1)),
 // r = sqrt(-2 log u1), (f0, f1) = r (sin v1, cos v1). Element i takes normal i % 4 of block
 // ctr0 + i / 4, as the uniform masks do.
+//
+// logf / sqrtf over the arguments Box-Muller reaches: box_muller_math.h.
 __device__ __forceinline__ void box_muller(uint32_t x0, uint32_t x1, float& f0, float& f1) {
-  float u1 = u01(x0);
-  if (u1 < 1.0e-7f) u1 = 1.0e-7f;
-  const float v1 = (float)(2.0 * 3.14159265358979323846 * (double)u01(x1));
-  const float r = sqrtf(-2.0f * logf(u1));
+  const float u1 = u01(x0);
+  const float v1 = efl_box_muller_angle(u01(x1));   // float(2 pi (double) u), no doubles
+  // both arms computed and one selected: a branch around the logarithm costs more than it saves
+  const float rr = sqrt_normal(-2.0f * log_unit(fmaxf(u1, 1.0e-7f)));
+  const float r = u1 < 1.0e-7f ? __uint_as_float(kRClampBits) : rr;
   float sn, cs;
   efl_sincos_angle(v1, &sn, &cs);   // v1 in [0, 2 pi]: <= 1 ulp of the rounded sin / cos (sincos_angle.h)
   f0 = sn * r;
@@ -231,6 +235,44 @@ __device__ __forceinline__ void normal4(uint64_t seed, uint64_t blk, float (&z)[
   philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
   box_muller(c[0], c[1], z[0], z[1]);
   box_muller(c[2], c[3], z[2], z[3]);
+}
+
+// The normals of NB blocks (blk0, blk0 + stride, ...), the same values as normal4 on each, computed
+// stage by stage across the 2 NB Box-Muller pairs (Philox rounds, logarithms, square roots, angles)
+// so that every stage has 2 NB independent chains to fill the transcendental and compare hazards
+// with (round 5: before, each pair ran to the end on its own, with s_nop between dependent steps).
+template <int NB>
+__device__ __forceinline__ void normals(uint64_t seed, uint64_t blk0, uint64_t stride, float (&z)[NB][4]) {
+  constexpr int P = 2 * NB;
+  uint32_t c[NB][4];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const uint64_t blk = blk0 + (uint64_t)b * stride;
+    c[b][0] = (uint32_t)blk;
+    c[b][1] = (uint32_t)(blk >> 32);
+    c[b][2] = 0u;
+    c[b][3] = 0u;
+  }
+  pl::philox_n<NB>(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  float u1[P], v1[P], r[P], sn[P], cs[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    u1[p] = u01(c[p >> 1][(p & 1) * 2]);
+    v1[p] = efl_box_muller_angle(u01(c[p >> 1][(p & 1) * 2 + 1]));
+  }
+#pragma unroll
+  for (int p = 0; p < P; ++p) r[p] = -2.0f * log_unit(fmaxf(u1[p], 1.0e-7f));
+#pragma unroll
+  for (int p = 0; p < P; ++p) r[p] = sqrt_normal(r[p]);
+#pragma unroll
+  for (int p = 0; p < P; ++p) r[p] = u1[p] < 1.0e-7f ? __uint_as_float(kRClampBits) : r[p];
+#pragma unroll
+  for (int p = 0; p < P; ++p) efl_sincos_angle(v1[p], &sn[p], &cs[p]);
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    z[p >> 1][(p & 1) * 2] = sn[p] * r[p];
+    z[p >> 1][(p & 1) * 2 + 1] = cs[p] * r[p];
+  }
 }
 
 // MODE 0, ElementWiseGaussianSumQuery.add_noise (dp_optimizer.py:70-71): v + normal * v * sigma;
@@ -258,15 +300,14 @@ __global__ __launch_bounds__(kBlock) void k_dp_noise(const float* x, float* o,  
     f4 v[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) v[b] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + g0 + b * kBlock);
+    float z[NB][4];
+    normals<NB>(seed, ctr0 + (uint64_t)g0, kBlock, z);
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-      const long long g = g0 + b * kBlock;
-      float z[4];
-      normal4(seed, ctr0 + (uint64_t)g, z);
       f4 r;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) r[j] = dp_one<MODE, POW2>(v[b][j], z[j], sigma, div);
-      stv(reinterpret_cast<f4*>(o) + g, r);
+      for (int j = 0; j < 4; ++j) r[j] = dp_one<MODE, POW2>(v[b][j], z[b][j], sigma, div);
+      stv(reinterpret_cast<f4*>(o) + g0 + b * kBlock, r);
     }
     return;
   }

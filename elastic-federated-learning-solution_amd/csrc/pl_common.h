@@ -14,20 +14,30 @@ struct Key {
 };
 
 // Philox4x32-10 (Salmon et al., SC'11): counter (ctr_lo, ctr_hi, block, 0), key = seed.
-__device__ __forceinline__ void philox(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
+// NB independent blocks advance round by round together (philox_n), so the chains interleave.
+template <int NB>
+__device__ __forceinline__ void philox_n(uint32_t (&c)[NB][4], uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
-    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
-    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
-    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
-    c[0] = n0;
-    c[1] = (uint32_t)p1;
-    c[2] = n2;
-    c[3] = (uint32_t)p0;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const uint64_t p0 = (uint64_t)0xD2511F53u * c[b][0];
+      const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[b][2];
+      // three-input XORs in one v_bitop3_b32 each (truth table 0x96); the compiler emits two v_xor
+      const uint32_t n0 = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c[b][1], k0, 0x96);
+      const uint32_t n2 = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c[b][3], k1, 0x96);
+      c[b][0] = n0;
+      c[b][1] = (uint32_t)p1;
+      c[b][2] = n2;
+      c[b][3] = (uint32_t)p0;
+    }
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
   }
+}
+
+__device__ __forceinline__ void philox(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
+  philox_n<1>(reinterpret_cast<uint32_t (&)[1][4]>(c), k0, k1);
 }
 
 // ---- the fixed-base exponent (FixedBasePowm, gmp_utils.cc:107-144) --------------------------

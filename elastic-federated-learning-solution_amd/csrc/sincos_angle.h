@@ -3,30 +3,49 @@
 // OCML's sincosf serves any float, so it carries a Payne-Hanek reduction for huge arguments; the
 // compiler flattens that path into selects (about 150 v_cndmask / v_alignbit / v_xor per lane of
 // the DP noise kernel, which made it VALU-bound at 0.57-0.68 of 8 TB/s). On [0, 2 pi] one
-// Cody-Waite step is exact enough: k = rint(v 2/pi) in 0..4, r = v - k pi/2 in double with pi/2 as a
-// double-double (an exact product in the FMA, |r| <= pi/4 + 2^-22, relative error < 2^-50 even for
-// the floats nearest to pi and 2 pi), r rounded to float once, then Cephes' single-precision
-// minimax polynomials for sin and cos on [-pi/4, pi/4] and the quadrant's sign/swap.
+// Cody-Waite step is exact enough: k = rint(v 2/pi) in 0..4, r = v - k pi/2 with pi/2 split into
+// three floats (C1 + C2 + C3, 72 bits; every step one fma), then Cephes' single-precision minimax
+// polynomials for sin and cos on [-pi/4, pi/4] and the quadrant's sign/swap. Round 3 reduced in
+// double (pi/2 as a double-double); round 5 does it in float: the reduced r is the same float for
+// every angle but one (float(pi/4) + 1 ulp, where v 2/pi rounds to 0.5 in float and k = 0 instead
+// of 1; sin there is now the correctly rounded one, 1 ulp off before), and the f64 conversions,
+// products and rint (4-cycle VALU on gfx950) go.
+//
+// efl_box_muller_angle(u) forms v1 = float(2 pi (double) u) without doubles: 2 pi (double) = A + B
+// in floats, u A exactly as p + e (fma), then p + (u B + e). The same float as the double product
+// for all 2^23 values of u (tests/test_sincos_angle.py checks them all).
 //
 // Accuracy is checked exhaustively on the host: tests/test_sincos_angle.py compiles this header
 // with gcc (-ffp-contract=off, the kernel file's own `fp contract(off)`; every fused step is an
-// explicit fma, so host and device round identically) and compares all 1.08e9 floats in [0, 2 pi]
-// with the correctly rounded sin / cos (double libm, rounded to float).
+// explicit fma, so host and device round identically) and compares every reachable angle and every
+// 61st float of [0, 2 pi] with the correctly rounded sin / cos (double libm, rounded to float).
 #pragma once
 
 #ifdef __HIPCC__
 #define EFL_SC_FN __host__ __device__ __forceinline__
+// every product and sum below rounds on its own wherever the header is included (hipcc contracts
+// a * b + c by default; p + (u b + e) fused would not be the double product)
+#define EFL_SC_NOCONTRACT _Pragma("clang fp contract(off)")
 #else
+#define EFL_SC_NOCONTRACT
 #include <math.h>
 #define EFL_SC_FN static inline
 #endif
 
+EFL_SC_FN float efl_box_muller_angle(float u) {
+  EFL_SC_NOCONTRACT
+  const float a = 0x1.921fb6p+2f, b = -0x1.777a5cp-23f;   // 2 pi (double) = a + b exactly
+  const float p = u * a;
+  const float e = fmaf(u, a, -p);                          // u a = p + e exactly
+  return p + fmaf(u, b, e);
+}
+
 EFL_SC_FN void efl_sincos_angle(float v, float* s, float* c) {
-  const double vd = (double)v;
-  const double k = rint(vd * 0.63661977236758134308);     // 2/pi
-  double rd = fma(-k, 1.5707963267948965580, vd);          // pi/2 high part
-  rd = fma(-k, 6.1232339957367658e-17, rd);                // pi/2 low part
-  const float r = (float)rd;
+  EFL_SC_NOCONTRACT
+  const float k = rintf(v * 0x1.45f306p-1f);               // 2/pi
+  float r = fmaf(-k, 0x1.921fb6p+0f, v);                   // pi/2 = C1 + C2 + C3
+  r = fmaf(-k, -0x1.777a5cp-25f, r);
+  r = fmaf(-k, -0x1.ee59dap-50f, r);
   const float z = r * r;
   float ps = fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f);
   ps = fmaf(ps, z, -1.6666654611e-1f);

@@ -6,6 +6,8 @@ Checked against the correctly rounded float of the double-precision libm sin / c
 * exhaustively over every angle the kernel can see, float(2 pi (double) u) for the 2^23 values
   u = j 2^-23 that Uint32ToFloat produces (TF's random_distributions.h, oracle/mask.py);
 * over every 61st float of [0, 2 pi] (about 18 M arguments), for any caller with another angle.
+Also exhaustively: efl_box_muller_angle(u) (the angle formed in floats) is the same float as
+float(2 pi (double) u) for all 2^23 u.
 The bound is 1 ulp for both (OCML's general sincosf, which the kernel used before, is also within
 1 ulp); the normal's stated tolerance in tests/test_dp_gpu.py (4 ulp) covers log, sqrt and the
 products on top of it.
@@ -35,6 +37,12 @@ static void check(float v) {
   if (dc > worst_c) worst_c = dc;
 }
 int main(void) {
+  long angle_differ = 0;
+  for (uint32_t j = 0; j < (1u << 23); ++j) {
+    const float u = (float)j * (1.0f / 8388608.0f);
+    if (efl_box_muller_angle(u) != (float)(2.0 * 3.14159265358979323846 * (double)u)) ++angle_differ;
+  }
+  printf("%ld\n", angle_differ);
   for (uint32_t j = 0; j < (1u << 23); ++j) {
     const float u = (float)j * (1.0f / 8388608.0f);
     check((float)(2.0 * 3.14159265358979323846 * (double)u));
@@ -66,11 +74,15 @@ def result(tmp_path_factory):
     return [tuple(int(v) for v in line.split()) for line in out if line.strip()]
 
 
+def test_angle_in_floats_is_the_double_product(result):
+    assert result[0] == (0,)
+
+
 def test_every_reachable_angle_within_1ulp(result):
-    ws, wc = result[0]
+    ws, wc = result[1]
     assert ws <= 1 and wc <= 1, f"sin {ws} ulp, cos {wc} ulp"
 
 
 def test_whole_range_sample_within_1ulp(result):
-    ws, wc = result[1]
+    ws, wc = result[2]
     assert ws <= 1 and wc <= 1, f"sin {ws} ulp, cos {wc} ulp"

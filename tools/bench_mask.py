@@ -30,6 +30,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--rows", type=int, default=65536)
 ap.add_argument("--cols", type=int, default=1024)
 ap.add_argument("--steps", type=int, default=50)
+ap.add_argument("--rounds", type=int, default=3, help="interleaved rounds over all kernels; the median is reported")
 ap.add_argument("--no-cpu-baseline", action="store_true")
 args = ap.parse_args()
 
@@ -91,22 +92,34 @@ def cpu_sample(name, rows=1024):
             "sample": f"[{rows}, {C}] fp32 slice, numpy oracle/mask.py (uniform + elementwise + concat), {reps} reps"}
 
 
-for name, (bpe, fn) in cases.items():
-    for _ in range(5):
-        efl.lib.check(fn())
-    torch.cuda.synchronize()
+def timed(fn):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
     for _ in range(args.steps):
         fn()
     e1.record(s)
     torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / args.steps
+    return e0.elapsed_time(e1) / args.steps
+
+
+for name, (bpe, fn) in cases.items():
+    for _ in range(5):
+        efl.lib.check(fn())
+torch.cuda.synchronize()
+# interleaved rounds: a box's clock drift over the run hits every kernel alike
+times = {name: [] for name in cases}
+for _ in range(args.rounds):
+    for name, (bpe, fn) in cases.items():
+        times[name].append(timed(fn))
+for name, (bpe, fn) in cases.items():
+    ms = float(np.median(times[name]))
     gbs = bpe * n / (ms * 1e-3) / 1e9
     line = {"kernel": name, "elements": n, "shape": [R, C], "ms": round(ms, 4),
+            "ms_rounds": [round(t, 4) for t in times[name]],
             "GiB_per_s_plaintext": round(4 * n / (ms * 1e-3) / 2**30, 2),
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_GBS, "unit": "GB/s",
-                         "frac": round(gbs / PEAK_GBS, 4), "bytes_per_elem": bpe}}
+                         "frac": round(gbs / PEAK_GBS, 4), "bytes_per_elem": bpe},
+            "library": efl.lib.version()}
     if not args.no_cpu_baseline and "_nb" not in name:
         line["cpu_baseline"] = cpu_sample(name)
     print(json.dumps(line), flush=True)

@@ -70,6 +70,12 @@ run() {
               -- python3 tools/crt_mnist_probe.py --parts 1 > gpurun_out/r05_crtkt.log 2>&1 ;;
     crtkt3) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r05_crtkt3 -o run --output-format csv \
               -- python3 tools/crt_mnist_probe.py --parts 3 > gpurun_out/r05_crtkt3.log 2>&1 ;;
+    dpchk)  hipcc --offload-arch=gfx950 -O3 -std=c++17 -I elastic-federated-learning-solution_amd/csrc \
+              tools/dp_fastmath_check.hip -o /tmp/dp_fastmath_check && \
+            timeout -k 10 60 /tmp/dp_fastmath_check > gpurun_out/r05_dp_fastmath.json 2>&1 ;;
+    mask)   timeout -k 10 300 python -u tools/bench_mask.py > gpurun_out/r05_bench_mask.jsonl 2> gpurun_out/r05_bench_mask.err ;;
+    masktests) timeout -k 10 600 python -u -m pytest tests/test_mask_gpu.py tests/test_secret_sharing_gpu.py tests/test_dp_gpu.py \
+              -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r05_mask_tests.log 2>&1 ;;
     crtkt2) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r05_crtkt2 -o run --output-format csv \
               -- python3 tools/crt_mnist_probe.py --n 262144 > gpurun_out/r05_crtkt2.log 2>&1 ;;
     profp)  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/r05_prof_p -o run --output-format csv \
