@@ -76,6 +76,8 @@ run() {
     mask)   timeout -k 10 300 python -u tools/bench_mask.py > gpurun_out/r05_bench_mask.jsonl 2> gpurun_out/r05_bench_mask.err ;;
     masktests) timeout -k 10 600 python -u -m pytest tests/test_mask_gpu.py tests/test_secret_sharing_gpu.py tests/test_dp_gpu.py \
               -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r05_mask_tests.log 2>&1 ;;
+    bprobe) BATCH_ARMS="base:512,2,512,2;k1:512,1,512,1;xcd:512,2,512,2,2,2;flat:512,2,512,2,1,1;persist:512,2,512,2,3,3,2048;persist4k:512,2,512,2,3,3,4096;b256k4:256,4,256,4;again:512,2,512,2" \
+              timeout -k 10 300 python -u tools/batched_probe.py > gpurun_out/r05_batched_probe.jsonl 2> gpurun_out/r05_batched_probe.err ;;
     crtkt2) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r05_crtkt2 -o run --output-format csv \
               -- python3 tools/crt_mnist_probe.py --n 262144 > gpurun_out/r05_crtkt2.log 2>&1 ;;
     profp)  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/r05_prof_p -o run --output-format csv \
