@@ -1027,6 +1027,16 @@ static int crt_run(efl_pl_ctx* c, const uint32_t* a, const int64_t* m, uint32_t*
   // ciphertext and no product mod n^2 is left (k_fbpowm28g); otherwise the walks start from the
   // key's R (y^2)^-1 and the join multiplies by g(m) mod n^2 (efl_pl_crt_join with the plaintext)
   bool direct = c->sub[0]->d.off_gn28 >= 0 && c->sub[1]->d.off_gn28 >= 0;
+  if (direct) {
+    // both walks as one list of waves when the one-lane family serves both sub-keys (round 5)
+    const Block& s0 = *c->sub[0];
+    const Block& s1 = *c->sub[1];
+    const int fam = efl_pl_tune(s0.ln, 0, -1);
+    const hipError_t e = pl::sl_crt_fbpowm2(pl::Key{s0.dev, s0.d}, pl::Key{s1.dev, s1.d}, fam > 0 ? fam : 0,
+                                            (const long long*)m, a, y[0], y[1], (long long)n, seed, (long long)ctr, s);
+    if (e == hipSuccess) return efl_pl_crt_join(mb.dev, &mb.d, y[0], y[1], nullptr, out, n, s);
+    if (e != hipErrorNotSupported) return hip_fail(e, "CRT walks");
+  }
   for (int i = 0; i < 2 && direct; ++i) {
     const Block& sb = *c->sub[i];
     const int fam = efl_pl_tune(sb.ln, 0, -1);

@@ -1721,6 +1721,211 @@ hipError_t run_fbpowm28g(const Key& k, const long long* m, const uint32_t* a, ui
   const hipError_t ferr = hipFreeAsync(st, s);
   return err != hipSuccess ? err : ferr;
 }
+// ---- the key owner's two CRT walks in one launch, last round split (round 5) ---------------------
+// The owner's encryption walks twice per element (mod p^2 and mod q^2, one lane each: family C = 32,
+// G = 1 for the examples' 1024-bit key). At the paillier_mnist activation that is 2 x 1,568 waves:
+// run per key, each launch leaves 480 of 1,024 SIMDs a wave short (1.53 per SIMD, 0.77 of the
+// lanes busy), and two streams do not help (3,136 waves still give 64 SIMDs a fourth). Here both
+// keys' walks are ONE list of waves: p's waves, then q's (a wave never mixes keys). The whole rounds
+// of that list (3,072 waves: 3 per SIMD) run as plain walks in one launch (k_crt_whole1); only the
+// waves past them (64) are split P ways over disjoint ranges of table rows (k_crt_part1, part 0
+// starting from the element's own start) and joined (k_crt_tjoin1), so the split's overhead (each
+// part draws and regroups a', the join's P - 1 products) is paid by 2 % of the walks, not all.
+// Same values, bit for bit, as the per-key walks (a product mod x^2 does not depend on its
+// grouping; every lazy part < 2 x^2 is a valid Montgomery operand).
+template <int C>
+__device__ __forceinline__ bool crt_wave(long long w, long long wpk, long long N, int lane, int& key, long long& el) {
+  key = w >= wpk ? 1 : 0;
+  el = (w - key * wpk) * kSlBlock + lane;
+  return el < N;
+}
+
+template <int C>
+__global__ __launch_bounds__(kSlBlock, EFL_WALK1_WAVES) void k_crt_whole1(
+    Key kp, Key kq, const uint32_t* __restrict__ a_in, const uint32_t* __restrict__ st0,
+    const uint32_t* __restrict__ st1, uint32_t* __restrict__ y0, uint32_t* __restrict__ y1, long long N,
+    long long wpk, uint64_t seed, long long ctr0) {
+  constexpr int L = C, E = kSlBlock;
+  constexpr int C28 = s28::limbs_per_lane(L, 1), CP = pad4<C28>();
+  extern __shared__ uint32_t lds[];
+  int key;
+  long long i;
+  if (!crt_wave<C>(blockIdx.x, wpk, N, (int)threadIdx.x, key, i)) return;
+  const Key& k = key ? kq : kp;
+  const int words = (k.d.a_bits + 31) >> 5;
+  uint32_t* B = lds + threadIdx.x;
+  uint32_t* A = lds + C28 * E + threadIdx.x;
+  if (a_in) {
+    for (int w = 0; w < words; ++w) A[w * E] = a_in[i * words + w];
+  } else {
+    draw_a<1>(A, E, words, k.d.a_bits, seed, (uint64_t)(ctr0 + i), 0);
+  }
+  lds_sync();
+  uint32_t h[C];
+  fbpowm28<C, 1>(h, k, A, B, E, words, 0, (key ? st1 : st0) + (size_t)i * CP);
+  store_slice<C>((key ? y1 : y0) + i * L, 0, h);
+}
+
+// part `part` of tail wave t (global wave w0 + t): slot v = (part * tw + t) * 64 + lane
+template <int C>
+__global__ __launch_bounds__(kSlBlock, EFL_WALK1_WAVES) void k_crt_part1(
+    Key kp, Key kq, const uint32_t* __restrict__ a_in, const uint32_t* __restrict__ st0,
+    const uint32_t* __restrict__ st1, uint32_t* __restrict__ P, unsigned char* __restrict__ F, long long N,
+    long long wpk, long long w0, long long tw, int parts, uint64_t seed, long long ctr0) {
+  constexpr int L = C, E = kSlBlock;
+  constexpr int C28 = s28::limbs_per_lane(L, 1), CP = pad4<C28>();
+  extern __shared__ uint32_t lds[];
+  const int part = (int)(blockIdx.x / tw);
+  const long long t = blockIdx.x - (long long)part * tw;
+  int key;
+  long long i;
+  if (!crt_wave<C>(w0 + t, wpk, N, (int)threadIdx.x, key, i)) return;
+  const Key& k = key ? kq : kp;
+  const long long v = (long long)blockIdx.x * kSlBlock + threadIdx.x;
+  const int words = (k.d.a_bits + 31) >> 5;
+  uint32_t* B = lds + threadIdx.x;
+  uint32_t* A = lds + C28 * E + threadIdx.x;
+  uint32_t m28[C28], acc[C28];
+  slice_uniform<C28>(m28, k.at(k.d.off_n2_28), 0);
+  bool have = false;
+  if (part == 0) {
+    const uint32_t* st = (key ? st1 : st0) + (size_t)i * CP;
+#pragma unroll
+    for (int j = 0; j < C28; ++j) acc[j] = st[j];
+    have = true;
+  }
+  if (a_in) {
+    for (int w = 0; w < words; ++w) A[w * E] = a_in[i * words + w];
+  } else {
+    draw_a<1>(A, E, words, k.d.a_bits, seed, (uint64_t)(ctr0 + i), 0);
+  }
+  lds_sync();
+  const int size = regroup_shared(A, E, words, k.d.group_size, 0);
+  const int rows = k.d.table_rows;
+  const int r0 = (int)((long long)rows * part / parts), r1 = (int)((long long)rows * (part + 1) / parts);
+  have = walk28_rows<C, 1>(acc, k, A, B, E, words, size, m28, 0, r0, r1, have);
+  store28<C28>(P + (size_t)v * CP, acc);
+  F[v] = have ? 1 : 0;
+}
+
+template <int C>
+__global__ __launch_bounds__(kSlBlock, EFL_WALK1_WAVES) void k_crt_tjoin1(
+    Key kp, Key kq, const uint32_t* __restrict__ P, const unsigned char* __restrict__ F, uint32_t* __restrict__ y0,
+    uint32_t* __restrict__ y1, long long N, long long wpk, long long w0, long long tw, int parts) {
+  constexpr int L = C, E = kSlBlock;
+  constexpr int C28 = s28::limbs_per_lane(L, 1), CP = pad4<C28>();
+  extern __shared__ uint32_t lds[];
+  int key;
+  long long i;
+  if (!crt_wave<C>(w0 + blockIdx.x, wpk, N, (int)threadIdx.x, key, i)) return;
+  const Key& k = key ? kq : kp;
+  uint32_t* B = lds + threadIdx.x;
+  uint32_t m28[C28], acc[C28];
+  slice_uniform<C28>(m28, k.at(k.d.off_n2_28), 0);
+  const uint32_t minv28 = k.d.n2_minv28;
+  load28<C28>(acc, P + ((size_t)blockIdx.x * kSlBlock + threadIdx.x) * CP);   // part 0: holds the start
+  for (int p = 1; p < parts; ++p) {
+    const long long v = ((long long)p * tw + blockIdx.x) * kSlBlock + threadIdx.x;
+    if (!F[v]) continue;
+    uint32_t b[C28];
+    load28<C28>(b, P + (size_t)v * CP);
+    s28::mul_fips1<C28>(acc, b, m28, minv28);
+  }
+  store_from_mont28<C, 1>((key ? y1 : y0) + i * L, acc, m28, minv28, B, E, 0);
+}
+
+// efl_pl_tune(ln, 5, v): the two-key CRT walks, 0 = chosen per launch (default), 1 = per key,
+// 2 = one list at every size (tests, A/B)
+std::atomic<int> g_crt_fused{0};
+constexpr int kMaxTailParts = 8;
+
+// Parts for the waves past the whole rounds: the P minimising (the tail's part rounds, each rows / P
+// + 1.5 products' time) + (the join: P - 1 products and the conversion, about 2), in walk units of
+// `rows` products; 1 = no split (the tail runs as plain walks, one more round). *cost = the whole
+// list's time in walk units.
+int tail_parts(long long waves, int rows, long long* whole, double* cost) {
+  const long long S = simd_count();
+  *whole = waves / S * S;
+  const long long tail = waves - *whole;
+  double best = tail ? 1.0 : 0.0;   // the unsplit tail: one more round
+  int bp = 1;
+  for (int P = 2; tail && rows >= 4 && P <= kMaxTailParts; ++P) {
+    const double part_rounds = (double)((tail * P + S - 1) / S);
+    const double c = part_rounds * ((double)rows / P + 1.5) / rows + (P + 1.0) / rows;
+    if (c < best * 0.97) {
+      best = c;
+      bp = P;
+    }
+  }
+  *cost = (double)(*whole / S) + best;
+  return bp;
+}
+
+// one list when it saves rounds against the per-key launches (2 ceil(waves per key / S)); with
+// equal rounds the per-key launches stay (each keeps one sub-key's table hot: 2 % at 262,144)
+bool crt_one_list(long long N, int rows, long long* whole, int* parts) {
+  const long long S = simd_count();
+  const long long wpk = (N + kSlBlock - 1) / kSlBlock;
+  double cost = 0.0;
+  *parts = tail_parts(2 * wpk, rows, whole, &cost);
+  if (*parts == 1) *whole = 2 * wpk;
+  return cost < 2.0 * (double)((wpk + S - 1) / S) * 0.97;
+}
+
+template <int C>
+hipError_t run_crt_walks1(const Key& kp, const Key& kq, const long long* m, const uint32_t* a, uint32_t* y0,
+                          uint32_t* y1, long long N, uint64_t seed, long long ctr0, hipStream_t s) {
+  constexpr int L = C, E = kSlBlock;
+  constexpr int C28 = s28::limbs_per_lane(L, 1), CP = pad4<C28>();
+  const long long wpk = (N + kSlBlock - 1) / kSlBlock, waves = 2 * wpk;
+  long long whole = 0;
+  int parts = 1;
+  if (kp.d.table_rows != kq.d.table_rows) return hipErrorNotSupported;   // the per-key launches (sl_fbpowm_g)
+  if (!crt_one_list(N, kp.d.table_rows, &whole, &parts) && g_crt_fused.load(std::memory_order_relaxed) != 2)
+    return hipErrorNotSupported;
+  const long long tw = waves - whole;
+  // scratch: both keys' starts, then the tail's parts and their flags
+  const size_t st_words = (size_t)wpk * kSlBlock * CP;
+  const size_t part_slots = (size_t)tw * parts * kSlBlock;
+  uint32_t* st = nullptr;
+  hipError_t err = hipMallocAsync(reinterpret_cast<void**>(&st), (2 * st_words + part_slots * CP) * 4 + part_slots, s);
+  if (err != hipSuccess) return err;
+  uint32_t* st0 = st;
+  uint32_t* st1 = st + st_words;
+  uint32_t* P = st + 2 * st_words;
+  unsigned char* F = reinterpret_cast<unsigned char*>(P + part_slots * CP);
+  const int aw = (kp.d.a_bits + 31) / 32;
+  const size_t lds0 = (size_t)(C28 > C ? C28 : C) * E * 4;
+  hipLaunchKernelGGL((k_gstart28<C, 1>), dim3(grid_of(N, 1)), dim3(kSlBlock), lds0, s, kp, m, st0, N);
+  err = hipGetLastError();
+  if (err == hipSuccess) {
+    hipLaunchKernelGGL((k_gstart28<C, 1>), dim3(grid_of(N, 1)), dim3(kSlBlock), lds0, s, kq, m, st1, N);
+    err = hipGetLastError();
+  }
+  const size_t lds = (size_t)(C28 + aw) * E * 4;
+  // the split tail after the whole rounds, on the same stream. Beside them on a second stream
+  // (forked and joined by events) it measured slower: the whole-round launch already keeps every
+  // SIMD busy, and at the MNIST activation it grew by 72 us, most of the 98 us the tail takes on its
+  // own (profiles/r05/crt_walks_two_streams.csv; Stage P 112 against 120 M encryptions/s)
+  if (err == hipSuccess && whole > 0) {
+    hipLaunchKernelGGL((k_crt_whole1<C>), dim3((unsigned)whole), dim3(kSlBlock), lds, s, kp, kq, a, st0, st1, y0, y1, N,
+                       wpk, seed, ctr0);
+    err = hipGetLastError();
+  }
+  if (err == hipSuccess && tw > 0) {
+    hipLaunchKernelGGL((k_crt_part1<C>), dim3((unsigned)(tw * parts)), dim3(kSlBlock), lds, s, kp, kq, a, st0, st1, P, F,
+                       N, wpk, whole, tw, parts, seed, ctr0);
+    err = hipGetLastError();
+    if (err == hipSuccess) {
+      hipLaunchKernelGGL((k_crt_tjoin1<C>), dim3((unsigned)tw), dim3(kSlBlock), (size_t)C28 * E * 4, s, kp, kq, P, F,
+                         y0, y1, N, wpk, whole, tw, parts);
+      err = hipGetLastError();
+    }
+  }
+  const hipError_t ferr = hipFreeAsync(st, s);
+  return err != hipSuccess ? err : ferr;
+}
+
 template <int C, int G, class XS>
 hipError_t run_powm28(const Key& k, const uint32_t* x, XS xs, uint32_t* out, long long N, unsigned long long* bad,
                       hipStream_t s) {
@@ -1910,6 +2115,18 @@ hipError_t sl_fbpowm_g(const Key& k, int C, const long long* m, const uint32_t* 
                        uint64_t seed, long long ctr0, hipStream_t s) {
   if (!C || !table28_for(k, C) || k.d.off_gn28 < 0 || k.d.off_gstart28 < 0) return hipErrorNotSupported;
   SL_DISPATCH(2 * k.d.ln, C, (run_fbpowm28g<CC, GG>(k, m, a, out, N, seed, ctr0, s)))
+}
+hipError_t sl_crt_fbpowm2(const Key& kp, const Key& kq, int C, const long long* m, const uint32_t* a, uint32_t* y0,
+                          uint32_t* y1, long long N, uint64_t seed, long long ctr0, hipStream_t s) {
+  if (g_crt_fused.load(std::memory_order_relaxed) == 1) return hipErrorNotSupported;
+  if (C != 32 || 2 * kp.d.ln != 32 || 2 * kq.d.ln != 32 || !table28_for(kp, C) || !table28_for(kq, C) ||
+      kp.d.off_gn28 < 0 || kp.d.off_gstart28 < 0 || kq.d.off_gn28 < 0 || kq.d.off_gstart28 < 0 ||
+      kp.d.a_bits != kq.d.a_bits || kp.d.group_size != kq.d.group_size)
+    return hipErrorNotSupported;
+  return run_crt_walks1<32>(kp, kq, m, a, y0, y1, N, seed, ctr0, s);
+}
+int sl_crt_fused(int v) {
+  return v < 0 ? g_crt_fused.load() : g_crt_fused.exchange(v);
 }
 hipError_t sl_add(const Key& k, int C, const uint32_t* x, const uint32_t* y, uint32_t* out, long long N,
                   hipStream_t s) {

@@ -326,7 +326,12 @@ int efl_pl_matmul(const void* key_block, const efl_pl_key* key, const uint32_t* 
  * (encryption with fresh randomness, efl_pl_fbpowm): a launch of fewer than 4 waves per SIMD splits
  * every element's walk over 1..5 disjoint ranges of table rows and joins the parts in a second
  * launch (stream-ordered scratch), so the waves fill the SIMDs; 0 = parts chosen per launch
- * (default), 1 = never split, 2..5 = that many, -1 queries. Results never change. */
+ * (default), 1 = never split, 2..5 = that many, -1 queries. decrypt = 5 sets how the key owner's
+ * CRT encryption (efl_pl_ctx_encrypt / efl_pl_ctx_fbpowm) runs its walks mod p^2 and mod q^2 when
+ * one lane holds each (1024-bit n): 0 = chosen per launch (default): both as one list of waves in
+ * one launch, the waves past its whole rounds split over table rows and joined, when that takes
+ * fewer rounds than one launch per sub-key; 1 = one launch per sub-key; 2 = one list at every size;
+ * -1 queries. Results never change. */
 int efl_pl_tune(int ln, int decrypt, int limbs_per_lane);
 
 /* ---- Key context: the PaillierKeypair resource ----------------------------------------------

@@ -78,6 +78,9 @@ run() {
               -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r05_mask_tests.log 2>&1 ;;
     bprobe) BATCH_ARMS="base:512,2,512,2;k1:512,1,512,1;xcd:512,2,512,2,2,2;flat:512,2,512,2,1,1;persist:512,2,512,2,3,3,2048;persist4k:512,2,512,2,3,3,4096;b256k4:256,4,256,4;again:512,2,512,2" \
               timeout -k 10 300 python -u tools/batched_probe.py > gpurun_out/r05_batched_probe.jsonl 2> gpurun_out/r05_batched_probe.err ;;
+    crtt)   timeout -k 10 600 python -u -m pytest tests/test_crt_walks_gpu.py tests/test_walk_split_gpu.py tests/test_paillier_crt_gpu.py \
+              tests/test_ctx_abi_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r05_crt_tests.log 2>&1 ;;
+    crtfp)  timeout -k 10 300 python -u tools/crt_fused_probe.py > gpurun_out/r05_crt_fused.jsonl 2> gpurun_out/r05_crt_fused.err ;;
     crtkt2) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r05_crtkt2 -o run --output-format csv \
               -- python3 tools/crt_mnist_probe.py --n 262144 > gpurun_out/r05_crtkt2.log 2>&1 ;;
     profp)  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/r05_prof_p -o run --output-format csv \
