@@ -1020,23 +1020,24 @@ EFL_API int efl_pl_ctx_copy(efl_pl_ctx* ctx, int which, int64_t off_words, int64
 static int crt_run(efl_pl_ctx* c, const uint32_t* a, const int64_t* m, uint32_t* out, int64_t n, uint64_t seed,
                    int64_t ctr, hipStream_t s) {
   const Block& mb = *c->main;
-  Scratch sc(s);
-  uint32_t* y[2] = {nullptr, nullptr};
-  for (int i = 0; i < 2; ++i) KS_HIP(sc.get((void**)&y[i], (size_t)n * c->sub[i]->lc * 4), "CRT scratch");
   // round 5: each walk starts from the element's (y^2)^-1 g(m), so the join of the two walks is the
   // ciphertext and no product mod n^2 is left (k_fbpowm28g); otherwise the walks start from the
   // key's R (y^2)^-1 and the join multiplies by g(m) mod n^2 (efl_pl_crt_join with the plaintext)
   bool direct = c->sub[0]->d.off_gn28 >= 0 && c->sub[1]->d.off_gn28 >= 0;
   if (direct) {
-    // both walks as one list of waves when the one-lane family serves both sub-keys (round 5)
+    // an element's two walks in one wave, joined at the end (round 5): the ciphertext in one pass
     const Block& s0 = *c->sub[0];
     const Block& s1 = *c->sub[1];
     const int fam = efl_pl_tune(s0.ln, 0, -1);
-    const hipError_t e = pl::sl_crt_fbpowm2(pl::Key{s0.dev, s0.d}, pl::Key{s1.dev, s1.d}, fam > 0 ? fam : 0,
-                                            (const long long*)m, a, y[0], y[1], (long long)n, seed, (long long)ctr, s);
-    if (e == hipSuccess) return efl_pl_crt_join(mb.dev, &mb.d, y[0], y[1], nullptr, out, n, s);
-    if (e != hipErrorNotSupported) return hip_fail(e, "CRT walks");
+    const hipError_t e = pl::sl_crt_encrypt_pair(pl::Key{s0.dev, s0.d}, pl::Key{s1.dev, s1.d}, fam > 0 ? fam : 0,
+                                                 mb.dev + mb.d.off_n2, (const long long*)m, a, out, (long long)n, seed,
+                                                 (long long)ctr, s);
+    if (e == hipSuccess) return EFL_OK;
+    if (e != hipErrorNotSupported) return hip_fail(e, "CRT encryption");
   }
+  Scratch sc(s);
+  uint32_t* y[2] = {nullptr, nullptr};
+  for (int i = 0; i < 2; ++i) KS_HIP(sc.get((void**)&y[i], (size_t)n * c->sub[i]->lc * 4), "CRT scratch");
   for (int i = 0; i < 2 && direct; ++i) {
     const Block& sb = *c->sub[i];
     const int fam = efl_pl_tune(sb.ln, 0, -1);

@@ -1444,9 +1444,9 @@ EFL_API int efl_pl_tune(int ln, int decrypt, int limbs_per_lane) {
     if (limbs_per_lane > 5) { set_error("walk parts must be 0 (auto) or 1..5"); return EFL_E_INVALID_ARGUMENT; }
     return pl::sl_walk_parts(limbs_per_lane);
   }
-  if (decrypt == 5) {   // the key owner's two CRT walks: 0 chosen per launch, 1 per key, 2 one list
+  if (decrypt == 5) {   // the key owner's CRT encryption: 0 chosen per launch, 1 per key, 2 paired lanes
     if (limbs_per_lane < 0) return pl::sl_crt_fused(-1);
-    if (limbs_per_lane > 2) { set_error("CRT walk mode must be 0 (chosen), 1 (per key) or 2 (one list)"); return EFL_E_INVALID_ARGUMENT; }
+    if (limbs_per_lane > 2) { set_error("CRT walk mode must be 0 (chosen), 1 (per key) or 2 (paired lanes)"); return EFL_E_INVALID_ARGUMENT; }
     return pl::sl_crt_fused(limbs_per_lane);
   }
   if (decrypt == 3) {   // efl_pl_matmul term splits: 0 chosen per launch, 1..16 fixed

@@ -1721,66 +1721,171 @@ hipError_t run_fbpowm28g(const Key& k, const long long* m, const uint32_t* a, ui
   const hipError_t ferr = hipFreeAsync(st, s);
   return err != hipSuccess ? err : ferr;
 }
-// ---- the key owner's two CRT walks in one launch, last round split (round 5) ---------------------
-// The owner's encryption walks twice per element (mod p^2 and mod q^2, one lane each: family C = 32,
-// G = 1 for the examples' 1024-bit key). At the paillier_mnist activation that is 2 x 1,568 waves:
-// run per key, each launch leaves 480 of 1,024 SIMDs a wave short (1.53 per SIMD, 0.77 of the
-// lanes busy), and two streams do not help (3,136 waves still give 64 SIMDs a fourth). Here both
-// keys' walks are ONE list of waves: p's waves, then q's (a wave never mixes keys). The whole rounds
-// of that list (3,072 waves: 3 per SIMD) run as plain walks in one launch (k_crt_whole1); only the
-// waves past them (64) are split P ways over disjoint ranges of table rows (k_crt_part1, part 0
-// starting from the element's own start) and joined (k_crt_tjoin1), so the split's overhead (each
-// part draws and regroups a', the join's P - 1 products) is paid by 2 % of the walks, not all.
-// Same values, bit for bit, as the per-key walks (a product mod x^2 does not depend on its
-// grouping; every lazy part < 2 x^2 is a valid Montgomery operand).
+// ---- the key owner's CRT encryption with an element's two walks in one wave (round 5) ------------
+// The owner's encryption walks twice per element, mod p^2 and mod q^2, one lane each (family C = 32,
+// G = 1 for the examples' 1024-bit key). Run per sub-key (k_gstart28 + k_fbpowm28 twice, then
+// efl_pl_crt_join), each launch of the paillier_mnist activation is 1,568 waves: 1.53 per SIMD, so
+// 480 of 1,024 SIMDs sit a wave short, and every launch pays its own tail. Here lanes 0-31 of a
+// wave walk elements 32 w .. 32 w + 31 mod p^2 and lanes 32-63 the same elements mod q^2 (a Key per
+// lane). Each lane makes its own walk start (y^2)^-1 g(m) first (what k_gstart28 writes, in
+// registers) and, after the walk, its half of the CRT join: q^2 y_p in the p lane, p^2 y_q in the q
+// lane (32 x 32 words each); the q lane hands its half to the p lane through LDS, which adds,
+// subtracts n^2 at most once and stores the ciphertext. One pass per element: no k_gstart28 or
+// join launch, no walk results in HBM. The list's whole rounds of waves run plain
+// (k_crt_pair_whole: 3,072 waves, 3 per SIMD, at the MNIST activation); only the waves past them
+// are split P ways over disjoint ranges of table rows (k_crt_pair_part, part 0 from the start) and
+// joined (k_crt_pair_tjoin), so the split's overhead (each part draws and regroups a', the join's
+// P - 1 products) falls on 2 % of the walks. Same values, bit for bit: a product mod x^2 does not
+// depend on its grouping, and every lazy part < 2 x^2 is a valid Montgomery operand.
+
+// the walk start of this lane's element: (y^2)^-1 g(m) R28 mod x^2 (k_gstart28's steps), B = this
+// lane's LDS column (C28 words at stride E)
 template <int C>
-__device__ __forceinline__ bool crt_wave(long long w, long long wpk, long long N, int lane, int& key, long long& el) {
-  key = w >= wpk ? 1 : 0;
-  el = (w - key * wpk) * kSlBlock + lane;
+__device__ __forceinline__ void lane_gstart(uint32_t (&acc)[s28::limbs_per_lane(C, 1)], const Key& k,
+                                            const uint32_t (&m28)[s28::limbs_per_lane(C, 1)], long long mi,
+                                            uint32_t* B, int E) {
+  constexpr int C28 = s28::limbs_per_lane(C, 1);
+  const uint32_t minv28 = k.d.n2_minv28;
+  const unsigned long long am = mi < 0 ? 0ull - (unsigned long long)mi : (unsigned long long)mi;
+  slice_uniform<C28>(acc, k.at(k.d.off_gn28), 0);
+  s28::mont_mul_steps<C28, 1>(acc, MLimbs{am}, m28, minv28, 0, 3);
+  to_lds<C28>(B, E, 0, acc);
+  lds_sync();
+  {
+    uint32_t t[C], x2[C];
+    s28::to_words<C>(t, B, E, C28, 0);
+    lds_sync();
+    slice_uniform<C>(x2, k.at(k.d.off_n2), 0);
+    csub<C, 1>(t, x2, geq<C, 1>(t, x2, 0), 0);
+    if (mi < 0) rsub<C, 1>(t, x2, 0);
+    add_small<C, 1>(t, 1u, 0);
+    to_lds<C>(B, E, 0, t);
+    lds_sync();
+  }
+  s28::from_words<C28>(acc, B, E, C, 0);
+  s28::mont_mul<C28, 1>(acc, Uniform{k.at(k.d.off_gstart28)}, m28, minv28, 0);
+}
+
+// z (2 L + 1 words) += f y for an L-word f (this lane's pointer) and a register L-word y, rows R
+// onwards (a template recursion, so every register index is a constant)
+template <int L, int R>
+__device__ __forceinline__ void add_rows(uint32_t (&z)[2 * L + 1], const uint32_t (&y)[L], const uint32_t* f,
+                                         uint32_t over = 0) {
+  if constexpr (R < L) {
+    const uint32_t fr = f[R];
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      const uint64_t p = (uint64_t)fr * y[j] + z[R + j] + c;
+      z[R + j] = (uint32_t)p;
+      c = (uint32_t)(p >> 32);
+    }
+    const uint64_t t = (uint64_t)z[R + L] + c + over;
+    z[R + L] = (uint32_t)t;
+    add_rows<L, R + 1>(z, y, f, (uint32_t)(t >> 32));
+  } else {
+    z[2 * L] += over;
+  }
+}
+
+// the CRT join from the two lanes of element el: h = this lane's walk (normal form, C words); the
+// p lane (q = false) ends with z = q^2 y_p + p^2 y_q - (n^2 if over) in out. Z = LDS area of
+// (2 C + 1) x 32 words (column = lane & 31). Every lane of the wave calls it (lanes past N too,
+// with el < 0: they only take part in the LDS order).
+template <int C>
+__device__ __forceinline__ void pair_join(const uint32_t (&h)[C], const uint32_t* other_x2, const uint32_t* n2w,
+                                          uint32_t* Z, uint32_t* out, bool q, bool valid) {
+  uint32_t z[2 * C + 1];
+#pragma unroll
+  for (int j = 0; j <= 2 * C; ++j) z[j] = 0u;
+  if (valid) add_rows<C, 0>(z, h, other_x2);
+  uint32_t* zc = Z + (threadIdx.x & 31);
+  if (q && valid) {
+#pragma unroll
+    for (int j = 0; j <= 2 * C; ++j) zc[j * 32] = z[j];
+  }
+  lds_sync();
+  if (q || !valid) return;
+  uint32_t c = 0;
+#pragma unroll
+  for (int j = 0; j <= 2 * C; ++j) {
+    const uint64_t s = (uint64_t)z[j] + zc[j * 32] + c;
+    z[j] = (uint32_t)s;
+    c = (uint32_t)(s >> 32);
+  }
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int j = 0; j < 2 * C; ++j) borrow = (uint32_t)(((uint64_t)z[j] - n2w[j] - borrow) >> 63);
+  const bool ge = z[2 * C] >= borrow;
+  borrow = 0;
+#pragma unroll
+  for (int j = 0; j < 2 * C; ++j) {
+    const uint64_t d = (uint64_t)z[j] - (ge ? n2w[j] : 0u) - borrow;
+    z[j] = (uint32_t)d;
+    borrow = (uint32_t)(d >> 63);
+  }
+  uint32_t zz[2 * C];
+#pragma unroll
+  for (int j = 0; j < 2 * C; ++j) zz[j] = z[j];
+  store_slice<2 * C>(out, 0, zz);
+}
+
+template <int C>
+__device__ __forceinline__ bool pair_lane(long long w, long long N, long long& el, bool& q) {
+  q = threadIdx.x >= 32;
+  el = w * 32 + (threadIdx.x & 31);
   return el < N;
 }
 
 template <int C>
-__global__ __launch_bounds__(kSlBlock, EFL_WALK1_WAVES) void k_crt_whole1(
-    Key kp, Key kq, const uint32_t* __restrict__ a_in, const uint32_t* __restrict__ st0,
-    const uint32_t* __restrict__ st1, uint32_t* __restrict__ y0, uint32_t* __restrict__ y1, long long N,
-    long long wpk, uint64_t seed, long long ctr0) {
-  constexpr int L = C, E = kSlBlock;
-  constexpr int C28 = s28::limbs_per_lane(L, 1), CP = pad4<C28>();
+__global__ __launch_bounds__(kSlBlock, EFL_WALK1_WAVES) void k_crt_pair_whole(
+    Key kp, Key kq, const uint32_t* __restrict__ n2w, const long long* __restrict__ m,
+    const uint32_t* __restrict__ a_in, uint32_t* __restrict__ out, long long N, uint64_t seed, long long ctr0) {
+  constexpr int E = kSlBlock, C28 = s28::limbs_per_lane(C, 1);
   extern __shared__ uint32_t lds[];
-  int key;
-  long long i;
-  if (!crt_wave<C>(blockIdx.x, wpk, N, (int)threadIdx.x, key, i)) return;
-  const Key& k = key ? kq : kp;
-  const int words = (k.d.a_bits + 31) >> 5;
-  uint32_t* B = lds + threadIdx.x;
-  uint32_t* A = lds + C28 * E + threadIdx.x;
-  if (a_in) {
-    for (int w = 0; w < words; ++w) A[w * E] = a_in[i * words + w];
-  } else {
-    draw_a<1>(A, E, words, k.d.a_bits, seed, (uint64_t)(ctr0 + i), 0);
+  long long el;
+  bool q;
+  const bool valid = pair_lane<C>(blockIdx.x, N, el, q);
+  const Key k = q ? kq : kp;
+  uint32_t h[C];
+  if (valid) {
+    const int words = (k.d.a_bits + 31) >> 5;
+    uint32_t* B = lds + threadIdx.x;
+    uint32_t* A = lds + C28 * E + threadIdx.x;
+    if (a_in) {
+      for (int w = 0; w < words; ++w) A[w * E] = a_in[el * words + w];
+    } else {
+      draw_a<1>(A, E, words, k.d.a_bits, seed, (uint64_t)(ctr0 + el), 0);
+    }
+    lds_sync();
+    uint32_t m28[C28], acc[C28];
+    slice_uniform<C28>(m28, k.at(k.d.off_n2_28), 0);
+    lane_gstart<C>(acc, k, m28, m ? m[el] : 0, B, E);
+    fbpowm28_walk<C, 1>(acc, k, A, B, E, words, m28, 0);
+    s28::mont_mul<C28, 1>(acc, Unit{}, m28, k.d.n2_minv28, 0);
+    lds_sync();
+    to_lds<C28>(B, E, 0, acc);
+    lds_sync();
+    s28::to_words<C>(h, B, E, C28, 0);
   }
   lds_sync();
-  uint32_t h[C];
-  fbpowm28<C, 1>(h, k, A, B, E, words, 0, (key ? st1 : st0) + (size_t)i * CP);
-  store_slice<C>((key ? y1 : y0) + i * L, 0, h);
+  const uint32_t* ox2 = q ? kp.at(kp.d.off_n2) : kq.at(kq.d.off_n2);   // the other prime's square
+  pair_join<C>(h, ox2, n2w, lds, out + el * 2 * C, q, valid);
 }
 
 // part `part` of tail wave t (global wave w0 + t): slot v = (part * tw + t) * 64 + lane
 template <int C>
-__global__ __launch_bounds__(kSlBlock, EFL_WALK1_WAVES) void k_crt_part1(
-    Key kp, Key kq, const uint32_t* __restrict__ a_in, const uint32_t* __restrict__ st0,
-    const uint32_t* __restrict__ st1, uint32_t* __restrict__ P, unsigned char* __restrict__ F, long long N,
-    long long wpk, long long w0, long long tw, int parts, uint64_t seed, long long ctr0) {
-  constexpr int L = C, E = kSlBlock;
-  constexpr int C28 = s28::limbs_per_lane(L, 1), CP = pad4<C28>();
+__global__ __launch_bounds__(kSlBlock, EFL_WALK1_WAVES) void k_crt_pair_part(
+    Key kp, Key kq, const long long* __restrict__ m, const uint32_t* __restrict__ a_in, uint32_t* __restrict__ P,
+    unsigned char* __restrict__ F, long long N, long long w0, long long tw, int parts, uint64_t seed, long long ctr0) {
+  constexpr int E = kSlBlock, C28 = s28::limbs_per_lane(C, 1), CP = pad4<C28>();
   extern __shared__ uint32_t lds[];
   const int part = (int)(blockIdx.x / tw);
   const long long t = blockIdx.x - (long long)part * tw;
-  int key;
-  long long i;
-  if (!crt_wave<C>(w0 + t, wpk, N, (int)threadIdx.x, key, i)) return;
-  const Key& k = key ? kq : kp;
+  long long el;
+  bool q;
+  if (!pair_lane<C>(w0 + t, N, el, q)) return;
+  const Key k = q ? kq : kp;
   const long long v = (long long)blockIdx.x * kSlBlock + threadIdx.x;
   const int words = (k.d.a_bits + 31) >> 5;
   uint32_t* B = lds + threadIdx.x;
@@ -1789,15 +1894,13 @@ __global__ __launch_bounds__(kSlBlock, EFL_WALK1_WAVES) void k_crt_part1(
   slice_uniform<C28>(m28, k.at(k.d.off_n2_28), 0);
   bool have = false;
   if (part == 0) {
-    const uint32_t* st = (key ? st1 : st0) + (size_t)i * CP;
-#pragma unroll
-    for (int j = 0; j < C28; ++j) acc[j] = st[j];
+    lane_gstart<C>(acc, k, m28, m ? m[el] : 0, B, E);
     have = true;
   }
   if (a_in) {
-    for (int w = 0; w < words; ++w) A[w * E] = a_in[i * words + w];
+    for (int w = 0; w < words; ++w) A[w * E] = a_in[el * words + w];
   } else {
-    draw_a<1>(A, E, words, k.d.a_bits, seed, (uint64_t)(ctr0 + i), 0);
+    draw_a<1>(A, E, words, k.d.a_bits, seed, (uint64_t)(ctr0 + el), 0);
   }
   lds_sync();
   const int size = regroup_shared(A, E, words, k.d.group_size, 0);
@@ -1809,33 +1912,43 @@ __global__ __launch_bounds__(kSlBlock, EFL_WALK1_WAVES) void k_crt_part1(
 }
 
 template <int C>
-__global__ __launch_bounds__(kSlBlock, EFL_WALK1_WAVES) void k_crt_tjoin1(
-    Key kp, Key kq, const uint32_t* __restrict__ P, const unsigned char* __restrict__ F, uint32_t* __restrict__ y0,
-    uint32_t* __restrict__ y1, long long N, long long wpk, long long w0, long long tw, int parts) {
-  constexpr int L = C, E = kSlBlock;
-  constexpr int C28 = s28::limbs_per_lane(L, 1), CP = pad4<C28>();
+__global__ __launch_bounds__(kSlBlock, EFL_WALK1_WAVES) void k_crt_pair_tjoin(
+    Key kp, Key kq, const uint32_t* __restrict__ n2w, const uint32_t* __restrict__ P,
+    const unsigned char* __restrict__ F, uint32_t* __restrict__ out, long long N, long long w0, long long tw,
+    int parts) {
+  constexpr int E = kSlBlock, C28 = s28::limbs_per_lane(C, 1), CP = pad4<C28>();
   extern __shared__ uint32_t lds[];
-  int key;
-  long long i;
-  if (!crt_wave<C>(w0 + blockIdx.x, wpk, N, (int)threadIdx.x, key, i)) return;
-  const Key& k = key ? kq : kp;
-  uint32_t* B = lds + threadIdx.x;
-  uint32_t m28[C28], acc[C28];
-  slice_uniform<C28>(m28, k.at(k.d.off_n2_28), 0);
-  const uint32_t minv28 = k.d.n2_minv28;
-  load28<C28>(acc, P + ((size_t)blockIdx.x * kSlBlock + threadIdx.x) * CP);   // part 0: holds the start
-  for (int p = 1; p < parts; ++p) {
-    const long long v = ((long long)p * tw + blockIdx.x) * kSlBlock + threadIdx.x;
-    if (!F[v]) continue;
-    uint32_t b[C28];
-    load28<C28>(b, P + (size_t)v * CP);
-    s28::mul_fips1<C28>(acc, b, m28, minv28);
+  long long el;
+  bool q;
+  const bool valid = pair_lane<C>(w0 + blockIdx.x, N, el, q);
+  const Key k = q ? kq : kp;
+  uint32_t h[C];
+  if (valid) {
+    uint32_t* B = lds + threadIdx.x;
+    uint32_t m28[C28], acc[C28];
+    slice_uniform<C28>(m28, k.at(k.d.off_n2_28), 0);
+    const uint32_t minv28 = k.d.n2_minv28;
+    load28<C28>(acc, P + ((size_t)blockIdx.x * kSlBlock + threadIdx.x) * CP);   // part 0: holds the start
+    for (int p = 1; p < parts; ++p) {
+      const long long v = ((long long)p * tw + blockIdx.x) * kSlBlock + threadIdx.x;
+      if (!F[v]) continue;
+      uint32_t b[C28];
+      load28<C28>(b, P + (size_t)v * CP);
+      s28::mul_fips1<C28>(acc, b, m28, minv28);
+    }
+    s28::mont_mul<C28, 1>(acc, Unit{}, m28, minv28, 0);
+    lds_sync();
+    to_lds<C28>(B, E, 0, acc);
+    lds_sync();
+    s28::to_words<C>(h, B, E, C28, 0);
   }
-  store_from_mont28<C, 1>((key ? y1 : y0) + i * L, acc, m28, minv28, B, E, 0);
+  lds_sync();
+  const uint32_t* ox2 = q ? kp.at(kp.d.off_n2) : kq.at(kq.d.off_n2);   // the other prime's square
+  pair_join<C>(h, ox2, n2w, lds, out + el * 2 * C, q, valid);
 }
 
-// efl_pl_tune(ln, 5, v): the two-key CRT walks, 0 = chosen per launch (default), 1 = per key,
-// 2 = one list at every size (tests, A/B)
+// efl_pl_tune(ln, 5, v): the key owner's CRT encryption, 0 = chosen per launch (the paired lanes
+// whenever they apply), 1 = one launch per sub-key and the join launch, 2 = the paired lanes
 std::atomic<int> g_crt_fused{0};
 constexpr int kMaxTailParts = 8;
 
@@ -1861,68 +1974,42 @@ int tail_parts(long long waves, int rows, long long* whole, double* cost) {
   return bp;
 }
 
-// one list when it saves rounds against the per-key launches (2 ceil(waves per key / S)); with
-// equal rounds the per-key launches stay (each keeps one sub-key's table hot: 2 % at 262,144)
-bool crt_one_list(long long N, int rows, long long* whole, int* parts) {
-  const long long S = simd_count();
-  const long long wpk = (N + kSlBlock - 1) / kSlBlock;
-  double cost = 0.0;
-  *parts = tail_parts(2 * wpk, rows, whole, &cost);
-  if (*parts == 1) *whole = 2 * wpk;
-  return cost < 2.0 * (double)((wpk + S - 1) / S) * 0.97;
-}
-
 template <int C>
-hipError_t run_crt_walks1(const Key& kp, const Key& kq, const long long* m, const uint32_t* a, uint32_t* y0,
-                          uint32_t* y1, long long N, uint64_t seed, long long ctr0, hipStream_t s) {
-  constexpr int L = C, E = kSlBlock;
-  constexpr int C28 = s28::limbs_per_lane(L, 1), CP = pad4<C28>();
-  const long long wpk = (N + kSlBlock - 1) / kSlBlock, waves = 2 * wpk;
+hipError_t run_crt_pair(const Key& kp, const Key& kq, const uint32_t* n2w, const long long* m, const uint32_t* a,
+                        uint32_t* out, long long N, uint64_t seed, long long ctr0, hipStream_t s) {
+  constexpr int E = kSlBlock, C28 = s28::limbs_per_lane(C, 1), CP = pad4<C28>();
+  const long long waves = (N + 31) / 32;
   long long whole = 0;
-  int parts = 1;
-  if (kp.d.table_rows != kq.d.table_rows) return hipErrorNotSupported;   // the per-key launches (sl_fbpowm_g)
-  if (!crt_one_list(N, kp.d.table_rows, &whole, &parts) && g_crt_fused.load(std::memory_order_relaxed) != 2)
-    return hipErrorNotSupported;
+  double cost = 0.0;
+  int parts = tail_parts(waves, kp.d.table_rows, &whole, &cost);
+  if (parts == 1) whole = waves;
   const long long tw = waves - whole;
-  // scratch: both keys' starts, then the tail's parts and their flags
-  const size_t st_words = (size_t)wpk * kSlBlock * CP;
-  const size_t part_slots = (size_t)tw * parts * kSlBlock;
-  uint32_t* st = nullptr;
-  hipError_t err = hipMallocAsync(reinterpret_cast<void**>(&st), (2 * st_words + part_slots * CP) * 4 + part_slots, s);
-  if (err != hipSuccess) return err;
-  uint32_t* st0 = st;
-  uint32_t* st1 = st + st_words;
-  uint32_t* P = st + 2 * st_words;
-  unsigned char* F = reinterpret_cast<unsigned char*>(P + part_slots * CP);
   const int aw = (kp.d.a_bits + 31) / 32;
-  const size_t lds0 = (size_t)(C28 > C ? C28 : C) * E * 4;
-  hipLaunchKernelGGL((k_gstart28<C, 1>), dim3(grid_of(N, 1)), dim3(kSlBlock), lds0, s, kp, m, st0, N);
+  // LDS: the walk's columns (C28 + aw words per lane), at least the join's (2 C + 1) x 32 words
+  const size_t walk_lds = (size_t)(C28 + aw) * E * 4, join_lds = (size_t)(2 * C + 1) * 32 * 4;
+  const size_t lds = walk_lds > join_lds ? walk_lds : join_lds;
+  hipError_t err = hipSuccess;
+  if (whole > 0) {
+    hipLaunchKernelGGL((k_crt_pair_whole<C>), dim3((unsigned)whole), dim3(kSlBlock), lds, s, kp, kq, n2w, m, a, out, N,
+                       seed, ctr0);
+    err = hipGetLastError();
+  }
+  if (err != hipSuccess || tw == 0) return err;
+  const size_t slots = (size_t)tw * parts * kSlBlock;
+  uint32_t* P = nullptr;
+  err = hipMallocAsync(reinterpret_cast<void**>(&P), slots * CP * 4 + slots, s);
+  if (err != hipSuccess) return err;
+  unsigned char* F = reinterpret_cast<unsigned char*>(P + slots * CP);
+  hipLaunchKernelGGL((k_crt_pair_part<C>), dim3((unsigned)(tw * parts)), dim3(kSlBlock), walk_lds, s, kp, kq, m, a, P, F,
+                     N, whole, tw, parts, seed, ctr0);
   err = hipGetLastError();
   if (err == hipSuccess) {
-    hipLaunchKernelGGL((k_gstart28<C, 1>), dim3(grid_of(N, 1)), dim3(kSlBlock), lds0, s, kq, m, st1, N);
+    const size_t tl = (size_t)C28 * E * 4 > join_lds ? (size_t)C28 * E * 4 : join_lds;
+    hipLaunchKernelGGL((k_crt_pair_tjoin<C>), dim3((unsigned)tw), dim3(kSlBlock), tl, s, kp, kq, n2w, P, F, out, N, whole,
+                       tw, parts);
     err = hipGetLastError();
   }
-  const size_t lds = (size_t)(C28 + aw) * E * 4;
-  // the split tail after the whole rounds, on the same stream. Beside them on a second stream
-  // (forked and joined by events) it measured slower: the whole-round launch already keeps every
-  // SIMD busy, and at the MNIST activation it grew by 72 us, most of the 98 us the tail takes on its
-  // own (profiles/r05/crt_walks_two_streams.csv; Stage P 112 against 120 M encryptions/s)
-  if (err == hipSuccess && whole > 0) {
-    hipLaunchKernelGGL((k_crt_whole1<C>), dim3((unsigned)whole), dim3(kSlBlock), lds, s, kp, kq, a, st0, st1, y0, y1, N,
-                       wpk, seed, ctr0);
-    err = hipGetLastError();
-  }
-  if (err == hipSuccess && tw > 0) {
-    hipLaunchKernelGGL((k_crt_part1<C>), dim3((unsigned)(tw * parts)), dim3(kSlBlock), lds, s, kp, kq, a, st0, st1, P, F,
-                       N, wpk, whole, tw, parts, seed, ctr0);
-    err = hipGetLastError();
-    if (err == hipSuccess) {
-      hipLaunchKernelGGL((k_crt_tjoin1<C>), dim3((unsigned)tw), dim3(kSlBlock), (size_t)C28 * E * 4, s, kp, kq, P, F,
-                         y0, y1, N, wpk, whole, tw, parts);
-      err = hipGetLastError();
-    }
-  }
-  const hipError_t ferr = hipFreeAsync(st, s);
+  const hipError_t ferr = hipFreeAsync(P, s);
   return err != hipSuccess ? err : ferr;
 }
 
@@ -2116,14 +2203,16 @@ hipError_t sl_fbpowm_g(const Key& k, int C, const long long* m, const uint32_t* 
   if (!C || !table28_for(k, C) || k.d.off_gn28 < 0 || k.d.off_gstart28 < 0) return hipErrorNotSupported;
   SL_DISPATCH(2 * k.d.ln, C, (run_fbpowm28g<CC, GG>(k, m, a, out, N, seed, ctr0, s)))
 }
-hipError_t sl_crt_fbpowm2(const Key& kp, const Key& kq, int C, const long long* m, const uint32_t* a, uint32_t* y0,
-                          uint32_t* y1, long long N, uint64_t seed, long long ctr0, hipStream_t s) {
+hipError_t sl_crt_encrypt_pair(const Key& kp, const Key& kq, int C, const uint32_t* n2w, const long long* m,
+                               const uint32_t* a, uint32_t* out, long long N, uint64_t seed, long long ctr0,
+                               hipStream_t s) {
   if (g_crt_fused.load(std::memory_order_relaxed) == 1) return hipErrorNotSupported;
   if (C != 32 || 2 * kp.d.ln != 32 || 2 * kq.d.ln != 32 || !table28_for(kp, C) || !table28_for(kq, C) ||
       kp.d.off_gn28 < 0 || kp.d.off_gstart28 < 0 || kq.d.off_gn28 < 0 || kq.d.off_gstart28 < 0 ||
-      kp.d.a_bits != kq.d.a_bits || kp.d.group_size != kq.d.group_size)
+      kp.d.a_bits != kq.d.a_bits || kp.d.group_size != kq.d.group_size || kp.d.table_rows != kq.d.table_rows ||
+      kp.d.table_window != kq.d.table_window || kp.d.table_cols != kq.d.table_cols)
     return hipErrorNotSupported;
-  return run_crt_walks1<32>(kp, kq, m, a, y0, y1, N, seed, ctr0, s);
+  return run_crt_pair<32>(kp, kq, n2w, m, a, out, N, seed, ctr0, s);
 }
 int sl_crt_fused(int v) {
   return v < 0 ? g_crt_fused.load() : g_crt_fused.exchange(v);

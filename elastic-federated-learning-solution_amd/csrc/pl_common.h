@@ -180,12 +180,14 @@ hipError_t sl_fbpowm(const Key& k, int C, const uint32_t* a, uint32_t* out, long
 // its radix-2^28 table does not serve family C
 hipError_t sl_fbpowm_g(const Key& k, int C, const long long* m, const uint32_t* a, uint32_t* out, long long N,
                        uint64_t seed, long long ctr0, hipStream_t s);
-// both CRT walks of the key owner's encryption in one list of waves, the waves past its whole
-// rounds split over table rows (one-lane family C = 32 only; hipErrorNotSupported otherwise, and
-// under efl_pl_tune(ln, 5, 1)): y0 = walk mod p^2, y1 = walk mod q^2, as sl_fbpowm_g gives them
-hipError_t sl_crt_fbpowm2(const Key& kp, const Key& kq, int C, const long long* m, const uint32_t* a, uint32_t* y0,
-                          uint32_t* y1, long long N, uint64_t seed, long long ctr0, hipStream_t s);
 int sl_crt_fused(int v);
+// the key owner's whole CRT encryption (or hs^(a') for m NULL) with an element's two walks in one
+// wave and the CRT join at its end: the ciphertext mod n^2 (n2w = n^2 in 32-bit words) into out
+// ([N][2 C] words). hipErrorNotSupported unless the one-lane family C = 32 serves both sub-keys
+// with equal tables (and under efl_pl_tune(ln, 5, 1))
+hipError_t sl_crt_encrypt_pair(const Key& kp, const Key& kq, int C, const uint32_t* n2w, const long long* m,
+                               const uint32_t* a, uint32_t* out, long long N, uint64_t seed, long long ctr0,
+                               hipStream_t s);
 hipError_t sl_add(const Key& k, int C, const uint32_t* x, const uint32_t* y, uint32_t* out, long long N,
                   hipStream_t s);
 hipError_t sl_powm(const Key& k, int C, const uint32_t* x, const uint32_t* e, int ew, uint32_t* out, long long N,

@@ -327,11 +327,11 @@ int efl_pl_matmul(const void* key_block, const efl_pl_key* key, const uint32_t* 
  * every element's walk over 1..5 disjoint ranges of table rows and joins the parts in a second
  * launch (stream-ordered scratch), so the waves fill the SIMDs; 0 = parts chosen per launch
  * (default), 1 = never split, 2..5 = that many, -1 queries. decrypt = 5 sets how the key owner's
- * CRT encryption (efl_pl_ctx_encrypt / efl_pl_ctx_fbpowm) runs its walks mod p^2 and mod q^2 when
- * one lane holds each (1024-bit n): 0 = chosen per launch (default): both as one list of waves in
- * one launch, the waves past its whole rounds split over table rows and joined, when that takes
- * fewer rounds than one launch per sub-key; 1 = one launch per sub-key; 2 = one list at every size;
- * -1 queries. Results never change. */
+ * CRT encryption (efl_pl_ctx_encrypt / efl_pl_ctx_fbpowm) runs when one lane holds each of its
+ * walks mod p^2 and mod q^2 (1024-bit n): 0 = chosen (default; the paired lanes whenever they
+ * apply), 1 = a walk launch per sub-key and the CRT join launch, 2 = the paired lanes: an element's
+ * two walks in one wave, its start made and its CRT join done in the same kernel, the waves past
+ * the launch's whole rounds split over table rows; -1 queries. Results never change. */
 int efl_pl_tune(int ln, int decrypt, int limbs_per_lane);
 
 /* ---- Key context: the PaillierKeypair resource ----------------------------------------------

@@ -1,5 +1,6 @@
-"""The key owner's CRT encryption with both walks as one list of waves (efl_pl_tune(16, 5, 0), the
-default) against one launch per sub-key (efl_pl_tune(16, 5, 1)), interleaved on one box, at the
+"""The key owner's CRT encryption per efl_pl_tune(16, 5, v) mode: 1 one launch per sub-key and the
+join launch, 2 an element's two walks in one wave with the join at its end (0, the default, picks
+2 where it applies), interleaved on one box, at the
 element counts the paillier_mnist layers use and around them. 1024-bit key (the examples'), HIP
 events on the launch stream. One JSON line per element count.
 
@@ -36,24 +37,26 @@ def main():
     for N in (4096, 32768, 50176, 100352, 131072, 262144):
         g = torch.Generator(device=dev).manual_seed(N)
         m = torch.randint(-2**40, 2**40, (N,), dtype=torch.int64, device=dev, generator=g)
-        t = {0: [], 1: []}
+        modes = (1, 2, 0)
+        t = {v: [] for v in modes}
         outs = {}
         for _ in range(a.rounds):
-            for mode in (0, 1):
-                lib.efl_pl_tune(16, 5, mode)
-                outs[mode] = owner.encrypt(m, counter_base=0).tensor.limbs
+            for v in modes:
+                lib.efl_pl_tune(16, 5, v)
+                outs[v] = owner.encrypt(m, counter_base=0).tensor.limbs
                 ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
                 ev[0].record(s)
                 for _ in range(a.reps):
                     owner.encrypt(m, counter_base=0)
                 ev[1].record(s)
                 ev[1].synchronize()
-                t[mode].append(ev[0].elapsed_time(ev[1]) / a.reps)
-        same = bool(torch.equal(outs[0], outs[1]))
-        m0, m1 = float(np.median(t[0])), float(np.median(t[1]))
-        print(json.dumps({"tool": "crt_fused_probe", "elements": N, "one_list_ms": round(m0, 4),
-                          "per_key_ms": round(m1, 4), "one_list_per_s": round(N / m0 * 1e3),
-                          "per_key_per_s": round(N / m1 * 1e3), "speedup": round(m1 / m0, 3),
+                t[v].append(ev[0].elapsed_time(ev[1]) / a.reps)
+        same = all(bool(torch.equal(outs[v], outs[1])) for v in modes)
+        ms = {v: float(np.median(t[v])) for v in modes}
+        print(json.dumps({"tool": "crt_fused_probe", "elements": N,
+                          "ms": {"per_key": round(ms[1], 4), "pair": round(ms[2], 4), "default": round(ms[0], 4)},
+                          "per_s": {"per_key": round(N / ms[1] * 1e3), "pair": round(N / ms[2] * 1e3),
+                                    "default": round(N / ms[0] * 1e3)},
                           "same_ciphertexts": same, "library": efl.lib.version()}), flush=True)
     lib.efl_pl_tune(16, 5, prev)
 
