@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 GPU session script: each GPU step under its own time limit, chained, output under
+# Round-5 GPU session script: each GPU step under its own time limit, chained, output under
 # gpurun_out/. Usage: bash tools/gpu_r05.sh <step>...
 set -o pipefail
 cd "$(dirname "$0")/.."
