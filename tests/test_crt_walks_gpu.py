@@ -103,3 +103,16 @@ def test_given_exponents(efl, owner):
     okp = P.Keypair(int(K1024["n"], 16), int(K1024["hs"], 16), 64, 10)
     for j in range(len(base)):
         assert f0[j] == P.hx(P.fbpowm(okp.hs, okp.n2, avals[j], 10)), j
+
+
+def test_extreme_plaintexts(efl, owner):
+    """int64 extremes and zero through the paired lanes' in-kernel starts ((1 +- |m| n) mod x^2 with
+    |m| up to 2^63): the per-key path's ciphertexts, and the plaintexts back."""
+    ext = [0, 1, -1, 2**63 - 1, -2**63, -2**63 + 1, 2**62, -2**62, 2**40, -2**40]
+    m = torch.tensor((ext * 500)[:4999], dtype=torch.int64, device="cuda")
+    out = {}
+    for v in (1, 2):
+        with mode(efl, v):
+            out[v] = owner.encrypt(m, counter_base=77)
+    assert torch.equal(out[1].tensor.limbs, out[2].tensor.limbs)
+    assert torch.equal(owner.decrypt(out[2], dtype=torch.int64), m)
