@@ -430,10 +430,14 @@ def stage_p_crt(k, subs, a_bytes, N, t, t_public, t_setup):
     issued = sum(_mont_macs(sk.desc.n2_28_len if sk.desc.off_table28 >= 0 else sk.lc, 0,
                             -(-8 * a_bytes // sk.table_window) * (1 - 2.0 ** -sk.table_window)) for sk in subs)
     per_s = N / t
+    from efl import lib as _l
+    paired = (subs[0].ln == 16 and pc_family(subs[0].ln) == 32 and _l.raw().efl_pl_tune(16, 5, -1) != 1)
+    route = ("an element's two walks in one wave, start and CRT join in the kernel, last round split"
+             if paired else "a walk launch per sub-key, then the CRT join launch")
     return {"elements_per_s": round(per_s), "ms": round(t * 1e3, 3), "vs_public_path": round(t_public / t, 3),
             "macs_per_element": int(macs),
-            "method": "(y^2)^-1 g(m) hs^a' mod p^2 and mod q^2 (W=%d/%d), CRT join = the ciphertext"
-                      % (subs[0].table_window, subs[1].table_window),
+            "method": "(y^2)^-1 g(m) hs^a' mod p^2 and mod q^2 (W=%d/%d), CRT join = the ciphertext; %s"
+                      % (subs[0].table_window, subs[1].table_window, route),
             "roofline": {"bound": "valu", "achieved": round(per_s * macs / 1e12, 3),
                          "peak": round(MAD_U64_U32_PEAK / 1e12, 3), "unit": "TMAC/s",
                          "frac": round(per_s * macs / MAD_U64_U32_PEAK, 4),
