@@ -189,14 +189,35 @@ def config3(efl, dev, steps, layout="separate"):
         torch.cuda.synchronize(dev)
         return (time.perf_counter() - t0) / k
 
+    for y in ys:
+        y.zero_()
     t_b = wall(batched, max(10, steps))
-    ok = all(torch.equal(x, y) for x, y in zip(xs[::64], ys[::64]))
+    # every slice compared bit for bit (FTZ: the identity on randn's bit patterns), on the device
+    ok = bool(torch.equal(torch.stack(xs).view(torch.int32), torch.stack(ys).view(torch.int32)))
+    # per-launch durations: a second pass with HIP events around each launch on the launch stream
+    reps = max(10, steps)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(reps)]
+    for e in evs:
+        e[0].record(stream)
+        efl.lib.encode_batched_into(enc_t, 1, False, sh)
+        e[1].record(stream)
+        efl.lib.decode_batched_into(dec_t, 1, flags, sh)
+        e[2].record(stream)
+    torch.cuda.synchronize(dev)
+    k_enc = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    k_dec = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    kbytes = BYTES_PER_ELEM_KERNEL * slices * elems
     nbytes = slices * elems * 4
     out = {"workload": f"config 3: 4096 x 64 KiB fp32 slices [128,128] ({layout}), batched encode+decode",
            "GiBs": round(nbytes / GIB / t_b, 2), "ms": round(t_b * 1e3, 4),
-           "hbm_frac": round(2 * BYTES_PER_ELEM_KERNEL * slices * elems / t_b / 1e9 / PEAK_HBM_GBS, 4),
+           "hbm_frac": round(2 * kbytes / t_b / 1e9 / PEAK_HBM_GBS, 4),
+           "kernels_ms": {"encode": round(k_enc, 4), "decode": round(k_dec, 4)},
+           "kernels_hbm_frac": {"encode": round(kbytes / (k_enc * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+                                "decode": round(kbytes / (k_dec * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)},
+           "tile_lanes_pairs": {"encode": list(efl.lib.batched_tile("encode")),
+                                "decode": list(efl.lib.batched_tile("decode"))},
            "table_entries": {"encode": enc_t.count, "decode": dec_t.count},
-           "launches": {"batched": 2}, "roundtrip_ok": ok}
+           "launches": {"batched": 2}, "roundtrip_ok": ok, "roundtrip_checked": "every slice, bit for bit"}
     if layout == "separate":
         t_n = wall(naive, 3)
         out.update({"naive_per_slice_ms": round(t_n * 1e3, 3), "naive_GiBs": round(nbytes / GIB / t_n, 3)})
@@ -765,13 +786,17 @@ def main(argv=None):
     torch.cuda.synchronize()
     t_enc = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))   # ms
     t_dec = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    # this rank's own kernel times and roofline fractions, before the max over ranks
+    own = edist.rank_kernel_report(t_enc, t_dec, elapsed / args.steps * 1e3, n, BYTES_PER_ELEM_KERNEL,
+                                   PEAK_HBM_GBS)
     if world > 1:
         elapsed, t_enc, t_dec = edist.all_reduce_max([elapsed, t_enc, t_dec])
 
     ms_per_step = elapsed / args.steps * 1e3
     value = world * (n * 4) / GIB / (elapsed / args.steps)
-    # every rank reports the device it really ran on (PCI location), gathered after the timed region
-    rank_devices = edist.gather_rank_devices(edist.rank_device_info(rank, dev))
+    # every rank reports the device it really ran on (PCI location) and its own kernel times,
+    # gathered after the timed region
+    rank_devices = edist.gather_rank_devices({**edist.rank_device_info(rank, dev), **own})
 
     # practical peak: device-to-device copy of the same byte volume as one kernel
     copy_gbs = None

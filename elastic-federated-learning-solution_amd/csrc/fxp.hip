@@ -303,8 +303,34 @@ struct DecF64Pair {
 // xcd_per > 0: XCD-aware tile order. Workgroups are dispatched round-robin over the 8 XCDs
 // (blockIdx % 8); workgroup b then takes tile (b % 8) * xcd_per + b / 8, so each XCD streams one
 // contiguous eighth of the tensor instead of every eighth tile (gridDim.x = 8 * xcd_per).
+// Kernel arguments as plain scalars (p0, p1, p2 = x, M, E for encode; M, E, y for decode), not the
+// Args struct: scalars can be preloaded into SGPRs at wave launch (the Makefile builds this file with
+// kernarg preload), and the empty asm below makes every argument the kernel reads arrive in one
+// scalar round trip otherwise. Passing the struct, the compiler loaded xcd_per, waited and branched,
+// then loaded nunits, waited and branched, then loaded the pointers: three dependent round trips
+// at the head of every workgroup before its first data load (round 6, from the ISA).
+template <class Args>
+__device__ __forceinline__ Args make_args(const void* p0, const void* p1, void* p2, int flag, int e_first) {
+  if constexpr (std::is_same<Args, EncArgs>::value) {
+    return EncArgs{p0, (long long*)p1, (long long*)p2, flag, e_first};
+  } else {
+    return DecArgs{(const long long*)p0, (const long long*)p1, p2, flag};
+  }
+}
+struct RawArgs {
+  const void* p0;
+  const void* p1;
+  void* p2;
+  int flag, e_first;
+};
+inline RawArgs raw_args(const EncArgs& a) { return {a.x, a.M, a.E, a.flag, a.e_first}; }
+inline RawArgs raw_args(const DecArgs& a) { return {a.M, a.E, a.y, a.flag, 0}; }
+
 template <class Op, int B, int K, int NT>
-__global__ __launch_bounds__(B) void k_stream(typename Op::Args a, long long nunits, int xcd_per) {
+__global__ __launch_bounds__(B) void k_stream(const void* p0, const void* p1, void* p2, int flag, int e_first,
+                                              long long nunits, int xcd_per) {
+  asm volatile("" ::"s"(p0), "s"(p1), "s"(p2), "s"(flag), "s"(e_first), "s"(nunits), "s"(xcd_per));
+  const typename Op::Args a = make_args<typename Op::Args>(p0, p1, p2, flag, e_first);
   const long long tile = (long long)B * K;
   const long long t0 = xcd_per > 0 ? (long long)(blockIdx.x & 7u) * xcd_per + (blockIdx.x >> 3) : blockIdx.x;
   for (long long base = t0 * tile; base < nunits;
@@ -347,18 +373,27 @@ __global__ __launch_bounds__(kBlock) void k_scalar(typename Op::Args a, long lon
 template <class Op, int B, int K, int NT>
 __device__ __forceinline__ void batched_tile(const void* const* src, void* const* dst0, void* const* dst1,
                                              const long long* ns, int flag, long long t, long long x) {
+  // All four table entries in one scalar round trip. Left alone, the compiler loads ns[t], waits,
+  // branches on it, and only then loads the three pointers: a second dependent L2 round trip at the
+  // head of every workgroup, which the streaming kernel does not pay (round 6: per-launch the
+  // batched kernels ran 4-6 % behind k_stream on the same contiguous bytes). The empty asm needs
+  // all four values in SGPRs, so the loads issue together and one s_waitcnt covers them.
   const long long n = ns[t];
+  const void* sp = src[t];
+  void* p0 = dst0[t];
+  void* p1 = dst1[t];
+  asm volatile("" ::"s"(n), "s"(sp), "s"(p0), "s"(p1));
   typename Op::Args a;
   if constexpr (std::is_same<typename Op::Args, EncArgs>::value) {
-    a = EncArgs{src[t], (long long*)dst0[t], (long long*)dst1[t], flag};
+    a = EncArgs{sp, (long long*)p0, (long long*)p1, flag};
   } else {
-    a = DecArgs{(const long long*)src[t], (const long long*)dst0[t], dst1[t], flag};
+    a = DecArgs{(const long long*)sp, (const long long*)p0, p1, flag};
   }
   const long long tile = (long long)B * K * Op::kElems;
   const long long e0 = x * tile;
   if (e0 >= n) return;
   // 16-B alignment of this tensor's streams decides vector vs element path (uniform branch).
-  const bool vec = aligned(src[t], 16) && aligned(dst0[t], 16) && aligned(dst1[t], 16);
+  const bool vec = aligned(sp, 16) && aligned(p0, 16) && aligned(p1, 16);
   const long long nunits = n / Op::kElems;
   const long long u0 = x * B * K;
   if (vec) {
@@ -555,12 +590,14 @@ constexpr int kEnc = 0, kDec = 1;
 // batched tile (efl_fxp_encode_batched / decode_batched): B lanes x K pairs per workgroup
 constexpr int kBatchB = 256, kBatchK = 4;
 constexpr long long kMaxGridY = 65535;
-// fp32 [encode, decode]: 512 lanes x 2 pairs both ways, one 2048-element tile per workgroup (half
-// the encode workgroups of round 2's 256 x 2 encode / 256 x 4 decode). Interleaved A/B on three
-// boxes (tools/batched_probe.py, profiles/r03/batched_probe_shapes.json): config-3 step 0.4086 ->
-// 0.4043, 0.4125 -> 0.4084 and 0.4319 -> 0.4390 ms, i.e. within the +-2 % box spread either way
+// fp32 [encode, decode]: encode 512 lanes x 1 pair (the streaming encode's tile, one 1024-element
+// tile per workgroup), decode 512 x 2. Rounds 3-5 ran 512 x 2 both ways; the per-launch A/B in one
+// process (tools/config3_coalesce_probe.py, profiles/r05/c3_coalesce.jsonl, c3_same_box.jsonl) put
+// the encode's 512 x 1 at -8 % on a slow box (0.2279 -> 0.2103 ms) and -0.5 % on a fast one, and the
+// decode's 512 x 2 ahead of 512 x 1 on the fast box (0.2007 against 0.2085 ms); round 6 re-took the
+// A/B interleaved (profiles/r06/c3_shapes.jsonl)
 std::atomic<int> g_batch_block[2] = {{512}, {512}};
-std::atomic<int> g_batch_k[2] = {{2}, {2}};
+std::atomic<int> g_batch_k[2] = {{1}, {2}};
 // efl_fxp_tune 17 / 18: tile order of the fp32 batched encode / decode: 0 2-D grid (tensor =
 // blockIdx.y), 1 one flat tensor-major grid, 2 the flat grid in XCD-aware order
 std::atomic<int> g_batch_order[2] = {{0}, {0}};
@@ -587,7 +624,9 @@ hipError_t launch_k(const typename Op::Args& a, long long nunits, hipStream_t s,
   }
   if (grid > 0x7FFFFFFFll) grid = 0x7FFFFFFFll;
   if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL((k_stream<Op, B, K, NT>), dim3((unsigned)grid), dim3(B), 0, s, a, nunits, xcd_per);
+  const RawArgs r = raw_args(a);
+  hipLaunchKernelGGL((k_stream<Op, B, K, NT>), dim3((unsigned)grid), dim3(B), 0, s, r.p0, r.p1, r.p2, r.flag,
+                     r.e_first, nunits, xcd_per);
   return hipGetLastError();
 }
 
@@ -735,6 +774,7 @@ EFL_API int efl_fxp_tune(int kind, int value) {
   }
   if (kind >= 10 && kind <= 13) {   // batched fp32: 10/11 encode block/K, 12/13 decode block/K
     const int dir = kind >= 12 ? kDec : kEnc;
+    if (value == -1) return kind % 2 == 0 ? g_batch_block[dir].load() : g_batch_k[dir].load();   // query
     if (kind % 2 == 0) {
       if (value != 128 && value != 256 && value != 512) return EFL_E_INVALID_ARGUMENT;
       return g_batch_block[dir].exchange(value);

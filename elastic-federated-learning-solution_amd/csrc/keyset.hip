@@ -21,6 +21,7 @@
 
 #include <memory>
 #include <mutex>
+#include <string>
 
 #include "common.h"
 #include "hostbig.h"
@@ -60,9 +61,13 @@ int64_t budget_left() {
   const int64_t b = budget_locked();
   return b > g_in_use ? b - g_in_use : 0;
 }
-void budget_take(int64_t bytes) {
+// reserve `bytes` only if they fit what is left, checked and taken under one lock: two contexts
+// setting keys at once on different threads cannot both size against the same remaining bytes
+bool budget_try_take(int64_t bytes) {
   std::lock_guard<std::mutex> g(g_budget_mu);
+  if (bytes > 0 && g_in_use + bytes > budget_locked()) return false;
   g_in_use += bytes;
+  return true;
 }
 void budget_give(int64_t bytes) {
   std::lock_guard<std::mutex> g(g_budget_mu);
@@ -171,6 +176,8 @@ struct Block {
   int64_t priv_off = 0, priv_words = 0;   // the private constants' reserved span of the head
   Big n, hs, n2, p, q, walk_start;
   bool has_walk = false, priv = false, has_table = false;
+  std::vector<uint32_t> head0;      // head and descriptor before the table was attached (drop_table)
+  efl_pl_key d0{};
   int a_bits = 0, g = 1, ln = 0, lc = 0, lh = 0;
   int W = 0, rows = 0, cols = 0, L28 = 0;   // the table's plan (L28 = 0: no radix-2^28 copy)
 
@@ -472,6 +479,13 @@ struct Scratch {   // stream-ordered device scratch, freed on the stream
 // column 0 = P[i][0] R, then pass k fills columns 2^k .. 2^(k+1) - 1 of every row at once as
 // column c times P[i][k] (efl_pl_add multiplies mod n^2: x R * y = x y R).
 int build_table(Block& b, hipStream_t s) {
+  // fault injection for the tests (tests/test_ctx_abi_gpu.py): a build that fails after upload()
+  // has already let the block's previous allocation go, as a scratch hipMallocAsync OOM would
+  const char* fail = getenv("EFL_PL_FAIL_TABLE_BUILD");
+  if (fail && fail[0] == '1' && fail[1] == 0) {
+    set_error("table build failed (EFL_PL_FAIL_TABLE_BUILD=1 fault injection)");
+    return EFL_E_RESOURCE_EXHAUSTED;
+  }
   const int lc = b.lc, W = b.W, rows = b.rows, cols = b.cols, L28 = b.L28;
   const int64_t hw = (int64_t)b.head.size();
   uint32_t* T = b.dev + hw;
@@ -586,15 +600,40 @@ int attach(Block& b, hipStream_t s) {
   return EFL_OK;
 }
 
-// head + table in one allocation, the table built now
+// head + table in one allocation, the table built now. The table's bytes are reserved in the
+// process budget first (atomically); on any failure the block is left with no device allocation.
 int realise_with_table(Block& b, hipStream_t s) {
   const int64_t tb = planned_table_bytes(b);
-  KS_RC(upload(b, true, s));
-  budget_take(tb);
+  if (!budget_try_take(tb)) {
+    set_error("Memory usage exceeds a predefined threshold. (the %lld-byte fixed-base table no longer fits the "
+              "table budget; efl_pl_table_budget)", (long long)tb);
+    return EFL_E_RESOURCE_EXHAUSTED;
+  }
+  b.head0 = b.head;
+  b.d0 = b.d;
+  const int rc0 = upload(b, true, s);
+  if (rc0 != EFL_OK) {
+    budget_give(tb);
+    return rc0;
+  }
   b.table_bytes = tb;
   int rc = build_table(b, s);
   if (rc == EFL_OK) rc = attach(b, s);
   if (rc != EFL_OK) b.release();
+  return rc;
+}
+
+// back to the table-less head in a fresh allocation (the table's bytes go back to the budget):
+// after a failed table build (whose upload had already let the old allocation go), or to hand a
+// key owner's unused n^2 table to its CRT sub-tables. The previous error text is kept.
+int drop_table(Block& b, hipStream_t s) {
+  if (!b.head0.empty()) {
+    b.head = b.head0;
+    b.d = b.d0;
+  }
+  const std::string err = efl_last_error();
+  const int rc = upload(b, false, s);
+  if (rc == EFL_OK) set_error("%s", err.c_str());
   return rc;
 }
 
@@ -675,6 +714,14 @@ int ensure_crt(efl_pl_ctx* c, hipStream_t s, bool* ok) {
     c->crt = -1;
     return EFL_OK;
   }
+  // A key that got its public half first (set_public, then set_private: the reference's usual order)
+  // built the n^2 table the owner's CRT encryption does not walk: it is released, so the sub-tables
+  // are sized against the whole budget as with efl_pl_set_keypair (W 18 -> 12 otherwise).
+  // An explicit window keeps it (the caller sized the tables).
+  if (c->main->has_table && !c->window) {
+    KS_RC(drop_table(*c->main, s));
+    ++c->generation;
+  }
   // the two sub-tables take half each of what the context may hold (round 4's split: W = 18 for the
   // examples' 1024-bit key under the 4 GiB default); the owner's own n^2 table, built only if the
   // public-key path is walked, is sized against what the budget has left then
@@ -752,6 +799,17 @@ int ensure_table(efl_pl_ctx* c, hipStream_t s) {
   }
   const int rc = realise_with_table(b, s);
   ++c->generation;
+  if (rc != EFL_OK) {
+    // the failed build had let the old allocation go: put the table-less head back, so every entry
+    // point still finds a live key block; if not even that works, the context holds no
+    // key ("No public key.") rather than a dangling block. The build's error is what is reported.
+    const std::string err = efl_last_error();
+    if (drop_table(b, s) != EFL_OK) {
+      c->drop_crt();
+      c->main.reset();
+    }
+    set_error("%s", err.c_str());
+  }
   return rc;
 }
 

@@ -1022,8 +1022,9 @@ __global__ __launch_bounds__(256) void k_to_int64(const uint32_t* __restrict__ m
 // dispatch
 // ------------------------------------------------------------------------------------------
 
-inline bool key_ok(const efl_pl_key* d, bool need_private, int ln_max) {
+inline bool key_ok(const void* kb, const efl_pl_key* d, bool need_private, int ln_max) {
   if (!d) { set_error("null key descriptor"); return false; }
+  if (!kb) { set_error("null key block"); return false; }   // e.g. a context whose table build failed
   if (d->a_bits <= 0 || d->a_bits > 8192) { set_error("a_bits must be in [1, 8192]"); return false; }
   if (d->ln != 16 && d->ln != 32 && d->ln != 64 && d->ln != 128 && d->ln != 256) {
     set_error("unsupported limb count %d (n of 512/1024/2048/4096/8192 bits)", d->ln);
@@ -1190,7 +1191,7 @@ using namespace efl;
 EFL_API int efl_pl_encrypt(const void* key_block, const efl_pl_key* key, const int64_t* plaintext,
                            const uint32_t* hsa, uint32_t* ciphertext, int64_t n, uint64_t seed,
                            int64_t counter_base, void* stream) {
-  if (!key_ok(key, false, 256)) return EFL_E_INVALID_ARGUMENT;
+  if (!key_ok(key_block, key, false, 256)) return EFL_E_INVALID_ARGUMENT;
   if (n < 0) { set_error("negative count"); return EFL_E_INVALID_ARGUMENT; }
   if (n == 0) return EFL_OK;
   if (!hsa) {
@@ -1208,7 +1209,7 @@ EFL_API int efl_pl_encrypt(const void* key_block, const efl_pl_key* key, const i
 
 EFL_API int efl_pl_fbpowm(const void* key_block, const efl_pl_key* key, const uint32_t* a, uint32_t* hsa,
                           int64_t n, uint64_t seed, int64_t counter_base, void* stream) {
-  if (!key_ok(key, false, 256)) return EFL_E_INVALID_ARGUMENT;
+  if (!key_ok(key_block, key, false, 256)) return EFL_E_INVALID_ARGUMENT;
   if (n <= 0) return n < 0 ? EFL_E_INVALID_ARGUMENT : EFL_OK;
   const int rc = table_ok(key);
   if (rc != EFL_OK) return rc;
@@ -1222,7 +1223,7 @@ EFL_API int efl_pl_fbpowm(const void* key_block, const efl_pl_key* key, const ui
 
 EFL_API int efl_pl_crt_join(const void* key_block, const efl_pl_key* key, const uint32_t* xp, const uint32_t* xq,
                             const int64_t* plaintext, uint32_t* z, int64_t n, void* stream) {
-  if (!key_ok(key, true, 256)) return key && !key->has_private ? EFL_E_ABORTED : EFL_E_INVALID_ARGUMENT;
+  if (!key_ok(key_block, key, true, 256)) return key && !key->has_private ? EFL_E_ABORTED : EFL_E_INVALID_ARGUMENT;
   if (n <= 0) return n < 0 ? EFL_E_INVALID_ARGUMENT : EFL_OK;
   Key k{(const uint32_t*)key_block, *key};
   hipStream_t s = (hipStream_t)stream;
@@ -1248,7 +1249,7 @@ EFL_API int efl_pl_crt_join(const void* key_block, const efl_pl_key* key, const 
 
 EFL_API int efl_pl_decrypt(const void* key_block, const efl_pl_key* key, const uint32_t* ciphertext,
                            uint32_t* magnitude, int8_t* negative, int64_t n, void* stream) {
-  if (!key_ok(key, true, 256)) return key && !key->has_private ? EFL_E_ABORTED : EFL_E_INVALID_ARGUMENT;
+  if (!key_ok(key_block, key, true, 256)) return key && !key->has_private ? EFL_E_ABORTED : EFL_E_INVALID_ARGUMENT;
   if (n < 0) { set_error("negative count"); return EFL_E_INVALID_ARGUMENT; }
   if (n == 0) return EFL_OK;
   Key k{(const uint32_t*)key_block, *key};
@@ -1268,7 +1269,7 @@ EFL_API int efl_pl_decrypt(const void* key_block, const efl_pl_key* key, const u
 
 EFL_API int efl_pl_add(const void* key_block, const efl_pl_key* key, const uint32_t* x, const uint32_t* y,
                        uint32_t* z, int64_t n, void* stream) {
-  if (!key_ok(key, false, 256)) return EFL_E_INVALID_ARGUMENT;
+  if (!key_ok(key_block, key, false, 256)) return EFL_E_INVALID_ARGUMENT;
   if (n <= 0) return n < 0 ? EFL_E_INVALID_ARGUMENT : EFL_OK;
   Key k{(const uint32_t*)key_block, *key};
   const int C = slicing(key->ln, 0);
@@ -1279,7 +1280,7 @@ EFL_API int efl_pl_add(const void* key_block, const efl_pl_key* key, const uint3
 
 EFL_API int efl_pl_powm(const void* key_block, const efl_pl_key* key, const uint32_t* x, const uint32_t* exps,
                         int exp_words, uint32_t* z, int64_t n, void* stream) {
-  if (!key_ok(key, false, 256)) return EFL_E_INVALID_ARGUMENT;
+  if (!key_ok(key_block, key, false, 256)) return EFL_E_INVALID_ARGUMENT;
   if (exp_words <= 0) { set_error("exp_words must be positive"); return EFL_E_INVALID_ARGUMENT; }
   if (n <= 0) return n < 0 ? EFL_E_INVALID_ARGUMENT : EFL_OK;
   Key k{(const uint32_t*)key_block, *key};
@@ -1319,8 +1320,8 @@ hipError_t powm_family<pl::ExpWords>(Key k, const uint32_t* x, pl::ExpWords xs, 
 }
 
 // common prologue of the ops with a device status word: argument checks, bad <- -1
-int status_prologue(const efl_pl_key* key, int64_t n, int64_t* bad, hipStream_t s, const char* op) {
-  if (!key_ok(key, false, 256)) return EFL_E_INVALID_ARGUMENT;
+int status_prologue(const void* key_block, const efl_pl_key* key, int64_t n, int64_t* bad, hipStream_t s, const char* op) {
+  if (!key_ok(key_block, key, false, 256)) return EFL_E_INVALID_ARGUMENT;
   if (!bad) { set_error("%s: null status word", op); return EFL_E_INVALID_ARGUMENT; }
   if (n < 0) { set_error("%s: negative count", op); return EFL_E_INVALID_ARGUMENT; }
   return hip_status(hipMemsetAsync(bad, 0xFF, sizeof(int64_t), s), op);
@@ -1331,7 +1332,7 @@ int status_prologue(const efl_pl_key* key, int64_t n, int64_t* bad, hipStream_t 
 EFL_API int efl_pl_mul_exp2(const void* key_block, const efl_pl_key* key, const uint32_t* x, const int64_t* y,
                             uint32_t* z, int64_t n, int64_t* bad, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  const int rc = status_prologue(key, n, bad, s, "efl_pl_mul_exp2");
+  const int rc = status_prologue(key_block, key, n, bad, s, "efl_pl_mul_exp2");
   if (rc != EFL_OK || n == 0) return rc;
   Key k{(const uint32_t*)key_block, *key};
   return hip_status(powm_family(k, x, pl::ExpPow2{(const long long*)y}, z, (long long)n, (unsigned long long*)bad, s),
@@ -1341,7 +1342,7 @@ EFL_API int efl_pl_mul_exp2(const void* key_block, const efl_pl_key* key, const 
 EFL_API int efl_pl_mul_scalar(const void* key_block, const efl_pl_key* key, const uint32_t* x, const int64_t* y,
                               uint32_t* z, int64_t n, int64_t* bad, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  const int rc = status_prologue(key, n, bad, s, "efl_pl_mul_scalar");
+  const int rc = status_prologue(key_block, key, n, bad, s, "efl_pl_mul_scalar");
   if (rc != EFL_OK || n == 0) return rc;
   Key k{(const uint32_t*)key_block, *key};
   unsigned long long* b = (unsigned long long*)bad;
@@ -1354,7 +1355,7 @@ EFL_API int efl_pl_mul_scalar_big(const void* key_block, const efl_pl_key* key, 
                                   const uint32_t* y_magnitude, int y_words, const int8_t* y_negative, uint32_t* z,
                                   int64_t n, int64_t* bad, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  const int rc = status_prologue(key, n, bad, s, "efl_pl_mul_scalar_big");
+  const int rc = status_prologue(key_block, key, n, bad, s, "efl_pl_mul_scalar_big");
   if (rc != EFL_OK || n == 0) return rc;
   if (y_words <= 0) { set_error("y_words must be positive"); return EFL_E_INVALID_ARGUMENT; }
   Key k{(const uint32_t*)key_block, *key};
@@ -1368,7 +1369,7 @@ EFL_API int efl_pl_fxp_add(const void* key_block, const efl_pl_key* key, const u
                            const uint32_t* y, const int64_t* y_exponent, uint32_t* z, int64_t n, int64_t* bad,
                            void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  const int rc = status_prologue(key, n, bad, s, "efl_pl_fxp_add");
+  const int rc = status_prologue(key_block, key, n, bad, s, "efl_pl_fxp_add");
   if (rc != EFL_OK || n == 0) return rc;
   Key k{(const uint32_t*)key_block, *key};
   unsigned long long* b = (unsigned long long*)bad;
@@ -1395,7 +1396,7 @@ EFL_API int efl_pl_fxp_add(const void* key_block, const efl_pl_key* key, const u
 
 EFL_API int efl_pl_invert(const void* key_block, const efl_pl_key* key, const uint32_t* x, uint32_t* z,
                           int64_t n, int64_t* bad, void* stream) {
-  if (!key_ok(key, false, 256)) return EFL_E_INVALID_ARGUMENT;
+  if (!key_ok(key_block, key, false, 256)) return EFL_E_INVALID_ARGUMENT;
   if (!bad) { set_error("null status word"); return EFL_E_INVALID_ARGUMENT; }
   hipStream_t s = (hipStream_t)stream;
   hipError_t e = hipMemsetAsync(bad, 0xFF, sizeof(int64_t), s);
@@ -1416,7 +1417,7 @@ EFL_API int efl_pl_matmul(const void* key_block, const efl_pl_key* key, const ui
                           const int64_t* x_exponent, const int64_t* y_mantissa, const int64_t* y_exponent,
                           uint32_t* z_pos, uint32_t* z_neg, int64_t* z_exponent, int u, int v, int w,
                           void* stream) {
-  if (!key_ok(key, false, 256)) return EFL_E_INVALID_ARGUMENT;
+  if (!key_ok(key_block, key, false, 256)) return EFL_E_INVALID_ARGUMENT;
   if (u < 0 || v <= 0 || w < 0) { set_error("bad matmul shape"); return EFL_E_INVALID_ARGUMENT; }
   if ((long long)u * w == 0) return EFL_OK;
   Key k{(const uint32_t*)key_block, *key};

@@ -1607,17 +1607,20 @@ hipError_t run_fbpowm(const Key& k, const uint32_t* a, uint32_t* out, long long 
                      out, N, seed, ctr0);
   return hipGetLastError();
 }
-// SIMDs of the current device (CUs x 4), read once
+// SIMDs of the current device (CUs x 4), read once per device index: a process that drives
+// several GPUs (or partition modes with different CU counts) sizes each device's splits by its own
+constexpr int kMaxDevices = 64;
 int simd_count() {
-  static std::atomic<int> n{0};
-  int v = n.load(std::memory_order_relaxed);
+  static std::atomic<int> n[kMaxDevices] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+  std::atomic<int>& slot = n[dev < kMaxDevices ? dev : kMaxDevices - 1];
+  int v = slot.load(std::memory_order_relaxed);
   if (!v) {
-    int dev = 0, cu = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cu <= 0)
-      cu = 256;
+    int cu = 0;
+    if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cu <= 0) cu = 256;
     v = 4 * cu;
-    n.store(v, std::memory_order_relaxed);
+    slot.store(v, std::memory_order_relaxed);
   }
   return v;
 }

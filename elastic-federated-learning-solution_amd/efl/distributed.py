@@ -101,6 +101,23 @@ def rank_device_info(rank: int, dev=None) -> dict:
     return info
 
 
+def rank_kernel_report(t_enc_ms: float, t_dec_ms: float, step_ms: float, elements: int,
+                       bytes_per_elem_kernel: int, peak_gbs: float) -> dict:
+    """This rank's OWN measurements, before any max over ranks: the per-launch encode / decode
+    durations (HIP events on its launch stream), its step time, and the HBM roofline fraction of
+    each kernel (algorithmic bytes = bytes_per_elem_kernel x elements per launch) and of its step.
+    Merged into its rank_device_info, so a multi-GPU line shows every GPU's own HBM fraction beside
+    the max-over-ranks step."""
+    kb = bytes_per_elem_kernel * elements
+
+    def frac(ms, nbytes):
+        return round(nbytes / (ms * 1e-3) / 1e9 / peak_gbs, 4) if ms > 0 else None
+    return {"kernels_ms": {"encode": round(t_enc_ms, 4), "decode": round(t_dec_ms, 4)},
+            "step_ms": round(step_ms, 4),
+            "roofline_frac": {"encode": frac(t_enc_ms, kb), "decode": frac(t_dec_ms, kb),
+                              "step": frac(step_ms, 2 * kb)}}
+
+
 def gather_rank_devices(info: dict, group=None) -> list:
     """Every rank's rank_device_info, in rank order, on every rank (all_gather_object; a single
     process returns [info])."""

@@ -406,6 +406,13 @@ def decode_batched_into(tables: BatchTables, dtype_code: int, flags=0, stream=No
     check(_lib.efl_fxp_decode_batched(src, d0, d1, dtype_code, ns, count, max_n, flags, stream))
 
 
+def batched_tile(direction: str):
+    """(lanes, pairs per lane) of the fp32 batched kernel of `direction` ("encode" / "decode"):
+    efl_fxp_tune kinds 10-13 read with value -1."""
+    k = 10 if direction == "encode" else 12
+    return _lib.efl_fxp_tune(k, -1), _lib.efl_fxp_tune(k + 1, -1)
+
+
 def fixed_point_to_float_point_batched(mantissas, exponents, dtype=torch.float32, flush_denormal=None):
     """One launch decoding a list of (mantissa, exponent) int64 device tensor pairs. Each pair is
     checked like efl_fxp_decode checks one (same size, fixed_point.cc:230-232) and made contiguous

@@ -80,6 +80,8 @@ const char* efl_last_error(void);
  * Philox blocks per lane of efl_dp_noise (1, 2, 4; default 4); kinds 21-24 = the fp64 encode's
  * workgroup size (128, 256, 512, 1024), units per lane (1, 2), nontemporal mask (as kind 4) and
  * XCD-aware tile order (0 / 1).
+ * Batched tile defaults (kinds 10-13): encode 512 lanes x 1 pair, decode 512 x 2; value -1 on
+ * kinds 10-13 reads the current value without changing it.
  * Returns the previous value or EFL_E_INVALID_ARGUMENT. */
 int efl_fxp_tune(int kind, int value);
 
@@ -392,7 +394,13 @@ int efl_pl_set_keypair(efl_pl_ctx* ctx, const char* n_hex, int n_bytes, const ch
 int efl_pl_set_private(efl_pl_ctx* ctx, const char* p_hex, const char* q_hex, void* stream);
 /* The key block and descriptor every efl_pl_* op above takes: which 0 = the key, 1 / 2 = the key
  * owner's CRT sub-keys (p, hs mod p^2) / (q, hs mod q^2) (after EFL_PL_PREPARE_CRT). ABORTED "No
- * public key." without one. Valid until the next set / prepare / destroy on ctx (see generation). */
+ * public key." without one. Valid until the next set / prepare / destroy on ctx — and until the next
+ * efl_pl_ctx_encrypt / efl_pl_ctx_fbpowm, which prepare implicitly: the first public-path call
+ * builds the deferred n^2 table into a new allocation, and the first key-owner call builds the CRT
+ * sub-keys and releases an n^2 table built before the private key arrived. Each such move bumps
+ * efl_pl_ctx_info.generation: a caller holding a block across calls re-fetches it when that changes.
+ * A failed table build leaves the previous table-less block in place (or no key at all), never a
+ * freed one; every efl_pl_* op refuses a null block. */
 int efl_pl_ctx_key(efl_pl_ctx* ctx, int which, const void** block, efl_pl_key* key);
 /* Build what a path needs ahead of use: EFL_PL_PREPARE_TABLE -> 1 (or RESOURCE_EXHAUSTED);
  * EFL_PL_PREPARE_CRT -> 1 sub-keys ready, 0 this key cannot take them (no private key, p q != n, no

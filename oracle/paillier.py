@@ -25,6 +25,16 @@ def _lib():
         L.pl_gmp_fbpowm.argtypes = [c, c, ctypes.c_uint, ctypes.c_uint, c, c, sz]
         L.pl_gmp_fbpowm.restype = i
         L.pl_gmp_powm.argtypes = [c, c, c, c, sz]
+        L.pl_gmp_add.argtypes = [c, c, c, c, sz]
+        L.pl_gmp_mul_scalar.argtypes = [c, c, c, c, sz]
+        L.pl_gmp_mul_scalar.restype = i
+        L.pl_gmp_mul_exp2.argtypes = [c, c, ctypes.c_longlong, c, sz]
+        L.pl_gmp_mul_exp2.restype = i
+        L.pl_gmp_invert.argtypes = [c, c, c, sz]
+        L.pl_gmp_invert.restype = i
+        vp = ctypes.c_void_p
+        L.pl_gmp_matmul.argtypes = [c, vp, vp, vp, vp, i, i, i, vp, sz, vp]
+        L.pl_gmp_matmul.restype = i
         L._pl_ready = True
     return L
 
@@ -64,6 +74,54 @@ def gmp_fbpowm(base: int, mod: int, exp_bits: int, g: int, a: int) -> int:
     if rc != 1:
         raise ValueError("exponent wider than the table")
     return int(b.value, 16)
+
+
+def gmp_add(n: int, x: int, y: int) -> str:                 # paillier.cc:157-169
+    b = _buf()
+    _lib().pl_gmp_add(hx(n).encode(), hx(x).encode(), hx(y).encode(), b, CAP)
+    return b.value.decode()
+
+
+def gmp_mul_scalar(n: int, x: int, y) -> str:               # paillier.cc:180-248
+    """y: a Python int (int32 / int64 / wider) or the signed hex text the string overload parses."""
+    b = _buf()
+    ys = y if isinstance(y, str) else hx(y)
+    if _lib().pl_gmp_mul_scalar(hx(n).encode(), hx(x).encode(), ys.encode(), b, CAP) != 0:
+        raise ValueError("x has no inverse mod n^2")
+    return b.value.decode()
+
+
+def gmp_mul_exp2(n: int, x: int, y: int) -> str:            # paillier.cc:722-733
+    b = _buf()
+    if _lib().pl_gmp_mul_exp2(hx(n).encode(), hx(x).encode(), y, b, CAP) != 0:
+        raise ValueError("y should be a positive tensor.")
+    return b.value.decode()
+
+
+def gmp_invert(n: int, x: int) -> str:                      # paillier.cc:275-285
+    b = _buf()
+    if _lib().pl_gmp_invert(hx(n).encode(), hx(x).encode(), b, CAP) != 0:
+        raise ValueError("x has no inverse mod n^2")
+    return b.value.decode()
+
+
+def gmp_matmul(n: int, xm, xe, ym, ye):                     # paillier.cc:987-1035
+    """xm [u][v] ciphertext ints, xe [u][v], ym / ye [v][w] ints -> (zm hex [u][w], ze [u][w])."""
+    u, v, w = len(xm), len(xm[0]), len(ym[0])
+    strs = [ctypes.create_string_buffer(hx(c).encode()) for row in xm for c in row]
+    xs = (ctypes.c_char_p * (u * v))(*[ctypes.cast(s, ctypes.c_char_p) for s in strs])
+    arr = ctypes.c_longlong * max(1, u * v)
+    xe_c = arr(*[e for row in xe for e in row])
+    yarr = ctypes.c_longlong * max(1, v * w)
+    ym_c = yarr(*[e for row in ym for e in row])
+    ye_c = yarr(*[e for row in ye for e in row])
+    out = ctypes.create_string_buffer(CAP * max(1, u * w))
+    ze = (ctypes.c_longlong * max(1, u * w))()
+    if _lib().pl_gmp_matmul(hx(n).encode(), xs, xe_c, ym_c, ye_c, u, v, w, out, CAP, ze) != 0:
+        raise ValueError("an x has no inverse mod n^2")
+    zm = [[out.raw[(i * w + k) * CAP:(i * w + k + 1) * CAP].split(b"\0", 1)[0].decode() for k in range(w)]
+          for i in range(u)]
+    return zm, [[ze[i * w + k] for k in range(w)] for i in range(u)]
 
 
 # ------------------------------------------------------------------ Python-int restatement

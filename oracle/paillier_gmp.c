@@ -10,6 +10,8 @@
  *   encrypt  PaillierKeypair::Encrypt             paillier.cc:103-131 (hsa given)
  *   decrypt  _Decrypt + m-function                paillier.cc:296-312, :39-48
  *   fbpowm   FixedBasePowm::init_table/mpz_fbpowm gmp_utils.cc:56-144
+ *   ops      Add / MulScalar / MulExp2 / Invert   paillier.cc:157-285, :722-733
+ *   matmul   PaillierMatmulOp::Compute            paillier.cc:987-1035
  * Strings are lowercase hex as mpz_get_str(..., 16) writes them (gmp_utils.cc:146-150).
  */
 #include <gmp.h>
@@ -209,6 +211,141 @@ EFL_EXPORT void pl_gmp_powm(const char* b_hex, const char* e_hex, const char* m_
   mpz_powm(r, b, e, m);
   put(out, cap, r);
   mpz_clears(b, e, m, r, NULL);
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Homomorphic ops through GMP in the reference's call order (known answers for tests/golden).
+ * Every ciphertext / scalar crosses as the hex text the TF ops carry (mpz_init_set_str(.., 16)).
+ * ------------------------------------------------------------------------------------------ */
+static void n_square(mpz_t n2, const char* n_hex) {
+  mpz_set_str(n2, n_hex, 16);
+  mpz_mul(n2, n2, n2);
+}
+
+/* PaillierKeypair::Add(string, string, string), paillier.cc:157-169 */
+EFL_EXPORT void pl_gmp_add(const char* n_hex, const char* x_hex, const char* y_hex, char* out, size_t cap) {
+  mpz_t n2, op, rop;
+  mpz_inits(n2, op, rop, NULL);
+  n_square(n2, n_hex);
+  mpz_set_str(rop, x_hex, 16);
+  mpz_set_str(op, y_hex, 16);
+  mpz_mul(rop, rop, op);
+  mpz_mod(rop, rop, n2);
+  put(out, cap, rop);
+  mpz_clears(n2, op, rop, NULL);
+}
+
+/* MulScalar(mpz x, mpz y, mpz z), paillier.cc:197-212: y < 0 inverts x mod n^2, then powm by |y|.
+ * The int64 and string overloads (:227-248) reach it with y = mpz_set_sll(y) / mpz_init_set_str(y,
+ * 16); the int32 overload (:180-195) computes the same value with powm_ui. y_hex is signed hex.
+ * Returns 0, or -1 when y < 0 and x has no inverse mod n^2 (the reference's result is undefined). */
+EFL_EXPORT int pl_gmp_mul_scalar(const char* n_hex, const char* x_hex, const char* y_hex, char* out, size_t cap) {
+  mpz_t n2, x, y, z, abs_y;
+  mpz_inits(n2, x, y, z, abs_y, NULL);
+  n_square(n2, n_hex);
+  mpz_set_str(x, x_hex, 16);
+  mpz_set_str(y, y_hex, 16);
+  int rc = 0;
+  if (mpz_sgn(y) < 0) {
+    mpz_neg(abs_y, y);
+    if (!mpz_invert(z, x, n2)) rc = -1;
+    else mpz_powm(z, z, abs_y, n2);
+  } else {
+    mpz_powm(z, x, y, n2);
+  }
+  if (!rc) put(out, cap, z);
+  mpz_clears(n2, x, y, z, abs_y, NULL);
+  return rc;
+}
+
+/* PaillierMulExp2Op::Compute per element, paillier.cc:722-733: y < 0 is an InvalidArgument
+ * (returns -1); else op = 2^y and MulScalar(x, op). */
+EFL_EXPORT int pl_gmp_mul_exp2(const char* n_hex, const char* x_hex, long long y, char* out, size_t cap) {
+  if (y < 0) return -1;
+  mpz_t n2, x, op, z;
+  mpz_inits(n2, x, op, z, NULL);
+  n_square(n2, n_hex);
+  mpz_set_str(x, x_hex, 16);
+  mpz_set_si(op, 1);
+  mpz_mul_2exp(op, op, (mp_bitcnt_t)y);
+  mpz_powm(z, x, op, n2);
+  put(out, cap, z);
+  mpz_clears(n2, x, op, z, NULL);
+  return 0;
+}
+
+/* Invert(string, string), paillier.cc:275-285. Returns -1 when x has no inverse mod n^2. */
+EFL_EXPORT int pl_gmp_invert(const char* n_hex, const char* x_hex, char* out, size_t cap) {
+  mpz_t n2, op;
+  mpz_inits(n2, op, NULL);
+  n_square(n2, n_hex);
+  mpz_set_str(op, x_hex, 16);
+  int rc = mpz_invert(op, op, n2) ? 0 : -1;
+  if (!rc) put(out, cap, op);
+  mpz_clears(n2, op, NULL);
+  return rc;
+}
+
+/* PaillierMatmulOp::Compute, paillier.cc:987-1035, statement for statement: y transposed into
+ * yt (:988-993), every x inverted mod n^2 (:994-999), then per output i the minimum exponent
+ * (:1006-1014) and per term MulScalar(x, y) for y >= 0 (:250-265 with y >= 0) or
+ * MulScalar(x^-1, -y) (:1020-1021), MulScalar by 2^(exp - min) (:1023-1025), and Add into the
+ * sum (:1026-1031). xs: u*v hex strings; xe [u][v]; ym, ye [v][w]; out: u*w strings of `cap`
+ * bytes each (row-major), ze [u][w]. Returns -1 if an x has no inverse. */
+EFL_EXPORT int pl_gmp_matmul(const char* n_hex, const char* const* xs, const long long* xe, const long long* ym,
+                             const long long* ye, int u, int v, int w, char* out, size_t cap, long long* ze) {
+  mpz_t n2, addend, e, sum;
+  mpz_inits(n2, addend, e, sum, NULL);
+  n_square(n2, n_hex);
+  const long long N = (long long)v * w;
+  long long* yt_m = (long long*)malloc(sizeof(long long) * (size_t)(N ? N : 1));
+  long long* yt_e = (long long*)malloc(sizeof(long long) * (size_t)(N ? N : 1));
+  for (long long i = 0; i < N; ++i) {
+    yt_m[i / w + i % w * v] = ym[i];
+    yt_e[i / w + i % w * v] = ye[i];
+  }
+  const long long NX = (long long)u * v;
+  mpz_t* xm = (mpz_t*)malloc(sizeof(mpz_t) * (size_t)(NX ? NX : 1));
+  mpz_t* xinv = (mpz_t*)malloc(sizeof(mpz_t) * (size_t)(NX ? NX : 1));
+  int rc = 0;
+  for (long long i = 0; i < NX; ++i) {
+    mpz_init_set_str(xm[i], xs[i], 16);
+    mpz_init(xinv[i]);
+    if (!mpz_invert(xinv[i], xm[i], n2)) rc = -1;
+  }
+  for (long long i = 0; rc == 0 && i < (long long)u * w; ++i) {
+    const long long sx = i / w * v, sy = i % w * v;
+    long long mn = 0x7FFFFFFFFFFFFFFFLL;
+    for (int j = 0; j < v; ++j) {
+      const long long ex = xe[sx + j] + yt_e[sy + j];
+      if (ex < mn) mn = ex;
+    }
+    for (int j = 0; j < v; ++j) {
+      const long long ex = xe[sx + j] + yt_e[sy + j] - mn;
+      const long long y = yt_m[sy + j];
+      const unsigned long long ay = y < 0 ? 0ull - (unsigned long long)y : (unsigned long long)y;
+      mpz_import(e, 1, -1, sizeof(ay), 0, 0, &ay);
+      mpz_powm(addend, y >= 0 ? xm[sx + j] : xinv[sx + j], e, n2);
+      mpz_set_si(e, 1);
+      mpz_mul_2exp(e, e, (mp_bitcnt_t)ex);
+      mpz_powm(addend, addend, e, n2);
+      if (!j) {
+        mpz_set(sum, addend);
+      } else {
+        mpz_mul(sum, addend, sum);
+        mpz_mod(sum, sum, n2);
+      }
+    }
+    ze[i] = mn;
+    put(out + (size_t)i * cap, cap, sum);
+  }
+  for (long long i = 0; i < NX; ++i) mpz_clears(xm[i], xinv[i], NULL);
+  free(xm);
+  free(xinv);
+  free(yt_m);
+  free(yt_e);
+  mpz_clears(n2, addend, e, sum, NULL);
+  return rc;
 }
 
 /* ------------------------------------------------------------------------------------------

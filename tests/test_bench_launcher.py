@@ -94,6 +94,32 @@ def test_rank_devices_gathered_over_gloo():
     for r, got in res:
         assert [d["rank"] for d in got] == [0, 1]
         assert all(d["device"] is None for d in got)
+        # every rank's own kernel times and roofline fractions travel with its entry (VERDICT r5
+        # item 6): rank 1 was given kernels twice as slow, and its fractions are its own
+        r0, r1 = got
+        assert r1["kernels_ms"]["encode"] == 2 * r0["kernels_ms"]["encode"]
+        assert abs(r0["roofline_frac"]["encode"] - 2 * r1["roofline_frac"]["encode"]) < 1e-3
+        for d in got:
+            assert set(d["roofline_frac"]) == {"encode", "decode", "step"}
+            assert d["step_ms"] > 0
+
+
+def test_rank_kernel_report_contract():
+    """rank_kernel_report: per-kernel fraction = bytes_per_elem x elements / kernel time / peak, the
+    step's = twice the bytes / step time; the field names bench.py and the SCALE reader rely on."""
+    sys.path.insert(0, os.path.join(ROOT, "elastic-federated-learning-solution_amd"))
+    from efl import distributed as edist
+    n = 65536 * 1024
+    r = edist.rank_kernel_report(0.2, 0.25, 0.45, n, 20, 8000.0)
+    assert r["kernels_ms"] == {"encode": 0.2, "decode": 0.25} and r["step_ms"] == 0.45
+    assert abs(r["roofline_frac"]["encode"] - 20 * n / 0.2e-3 / 8e12) < 1e-4
+    assert abs(r["roofline_frac"]["decode"] - 20 * n / 0.25e-3 / 8e12) < 1e-4
+    assert abs(r["roofline_frac"]["step"] - 40 * n / 0.45e-3 / 8e12) < 1e-4
+    assert edist.rank_kernel_report(0.0, 0.1, 0.1, n, 20, 8000.0)["roofline_frac"]["encode"] is None
+    src = open(BENCH).read()
+    assert "edist.gather_rank_devices({**edist.rank_device_info(rank, dev), **own})" in src
+    # the report is taken before the max over ranks overwrites this rank's times
+    assert src.index("own = edist.rank_kernel_report(") < src.index("edist.all_reduce_max([elapsed, t_enc, t_dec])")
 
 
 def _free_port():
@@ -109,7 +135,8 @@ def _gather_worker(rank, world, port, q):
     from efl import distributed as edist
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
-        q.put((rank, edist.gather_rank_devices(edist.rank_device_info(rank, None))))
+        own = edist.rank_kernel_report(0.2 * (rank + 1), 0.2 * (rank + 1), 0.4 * (rank + 1), 1 << 26, 20, 8000.0)
+        q.put((rank, edist.gather_rank_devices({**edist.rank_device_info(rank, None), **own})))
     finally:
         dist.destroy_process_group()
 
@@ -131,6 +158,11 @@ def test_gpus2_launches_two_ranks_on_one_gpu():
     assert [d["rank"] for d in rd] == [0, 1]
     assert all(d["device"] == 0 and d["pci"] for d in rd)
     assert len({(d["host"], d["pci"]) for d in rd}) == 1
+    # each rank's own kernel times and HBM fractions (two ranks share the card, so each is slower
+    # than alone, but each ran its kernels and reports them)
+    for d in rd:
+        assert d["kernels_ms"]["encode"] > 0 and d["kernels_ms"]["decode"] > 0 and d["step_ms"] > 0
+        assert 0 < d["roofline_frac"]["encode"] < 1 and 0 < d["roofline_frac"]["step"] < 1
     # value = 2 x 0.25 GiB per step / max-over-ranks step time; the K timed steps fit in the wall
     assert out["value"] > 0 and out["steps"] * out["ms_per_step"] * 1e-3 < wall
     assert abs(out["value"] - 2 * 0.25 / (out["ms_per_step"] * 1e-3)) / out["value"] < 0.01

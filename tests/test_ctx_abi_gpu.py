@@ -212,3 +212,93 @@ def test_process_wide_table_budget(lib):
         for c in ctxs:
             c.close()
         lib.efl_pl_table_budget(prev, None)
+
+
+def _info(lib, c):
+    info = (ctypes.c_char * 256)()
+    ok(lib, lib.efl_pl_ctx_query(c.h, info))
+    b = bytes(info)
+
+    def i32_at(o):
+        return int.from_bytes(b[o:o + 4], "little", signed=True)
+
+    def i64_at(o):
+        return int.from_bytes(b[o:o + 8], "little", signed=True)
+    return {"table_window": i32_at(24), "has_table": i32_at(28), "crt": i32_at(36),
+            "crt_table_window": [i32_at(40), i32_at(44)], "table_bytes": i64_at(56), "generation": i64_at(104)}
+
+
+def test_failed_table_build_leaves_a_live_key(lib, monkeypatch):
+    """a deferred n^2 table build that fails after the block was re-uploaded must
+    not leave the context with a freed key block. With the build forced to fail
+    (EFL_PL_FAIL_TABLE_BUILD=1), the public-path encryption returns RESOURCE_EXHAUSTED; then
+    decryption, the CRT encryption and, once the build succeeds, the public path all give the right
+    answers. The stateless ops refuse a null key block instead of faulting."""
+    k = KEYS[0]
+    ln = k["n_bytes"] // 4
+    c = Ctx(lib)
+    try:
+        lib.efl_pl_set_keypair.argtypes = [vp, cp, i32, cp, i32, i32, cp, cp, vp]
+        ok(lib, lib.efl_pl_set_keypair(c.h, k["n"].encode(), k["n_bytes"], k["hs"].encode(), k["a_bits"] // 8, 1,
+                                       k["p"].encode(), k["q"].encode(), stream()))
+        assert _info(lib, c)["has_table"] == 0                     # the owner's n^2 table is deferred
+        N = 64
+        m = torch.randint(-2**40, 2**40, (N,), dtype=torch.int64, device="cuda")
+        ct = torch.empty((N, 2 * ln), dtype=torch.int32, device="cuda")
+        monkeypatch.setenv("EFL_PL_FAIL_TABLE_BUILD", "1")
+        rc = lib.efl_pl_ctx_encrypt(c.h, m.data_ptr(), None, ct.data_ptr(), N, 5, 0, 1, stream())
+        assert rc == -8 and b"fault injection" in lib.efl_last_error()
+        assert lib.efl_pl_ctx_prepare(c.h, 1, stream()) == -8
+        assert _info(lib, c)["has_table"] == 0
+        mag = torch.empty((N, ln), dtype=torch.int32, device="cuda")
+        neg = torch.empty(N, dtype=torch.int8, device="cuda")
+        # the CRT route and decryption still run on the live block
+        ok(lib, lib.efl_pl_ctx_encrypt(c.h, m.data_ptr(), None, ct.data_ptr(), N, 5, 0, 0, stream()))
+        ok(lib, lib.efl_pl_ctx_decrypt(c.h, ct.data_ptr(), mag.data_ptr(), neg.data_ptr(), N, stream()))
+        assert [(-x if s else x) for x, s in zip(ints(mag), neg.cpu().tolist())] == m.cpu().tolist()
+        monkeypatch.delenv("EFL_PL_FAIL_TABLE_BUILD")
+        ct2 = torch.empty_like(ct)
+        ok(lib, lib.efl_pl_ctx_encrypt(c.h, m.data_ptr(), None, ct2.data_ptr(), N, 5, 0, 1, stream()))
+        assert torch.equal(ct2, ct) and _info(lib, c)["has_table"] == 1
+        # a null key block is refused by every stateless entry point
+        blk, desc = vp(), ctypes.create_string_buffer(DESC_BYTES)
+        ok(lib, lib.efl_pl_ctx_key(c.h, 0, ctypes.byref(blk), desc))
+        assert lib.efl_pl_decrypt(None, desc, ct.data_ptr(), mag.data_ptr(), neg.data_ptr(), N, stream()) == -3
+        assert b"null key block" in lib.efl_last_error()
+        assert lib.efl_pl_encrypt(None, desc, m.data_ptr(), None, ct.data_ptr(), N, 0, 0, stream()) == -3
+    finally:
+        c.close()
+
+
+def test_public_then_private_gives_crt_the_whole_budget(lib):
+    """the reference's usual order (SetPaillierPublicKey, then SetPaillierPrivateKey). The
+    public step builds the n^2 table; the owner's first encryption builds the CRT sub-keys and
+    releases that table, so the sub-tables get the windows efl_pl_set_keypair gives them (not the
+    few MB the n^2 table left), and the ciphertexts are the public path's."""
+    k = KEYS[0]
+    ln = k["n_bytes"] // 4
+    a, b = Ctx(lib), Ctx(lib)
+    try:
+        lib.efl_pl_set_keypair.argtypes = [vp, cp, i32, cp, i32, i32, cp, cp, vp]
+        ok(lib, lib.efl_pl_set_keypair(a.h, k["n"].encode(), k["n_bytes"], k["hs"].encode(), k["a_bits"] // 8, 1,
+                                       k["p"].encode(), k["q"].encode(), stream()))
+        assert lib.efl_pl_ctx_prepare(a.h, 2, stream()) == 1
+        want = _info(lib, a)["crt_table_window"]
+        a.close()
+        ok(lib, lib.efl_pl_set_public(b.h, k["n"].encode(), k["n_bytes"], k["hs"].encode(), k["a_bits"] // 8, 1,
+                                      stream()))
+        assert _info(lib, b)["has_table"] == 1
+        ok(lib, lib.efl_pl_set_private(b.h, k["p"].encode(), k["q"].encode(), stream()))
+        N = 128
+        m = torch.randint(-2**40, 2**40, (N,), dtype=torch.int64, device="cuda")
+        c1 = torch.empty((N, 2 * ln), dtype=torch.int32, device="cuda")
+        c2 = torch.empty_like(c1)
+        ok(lib, lib.efl_pl_ctx_encrypt(b.h, m.data_ptr(), None, c1.data_ptr(), N, 9, 3, 0, stream()))
+        inf = _info(lib, b)
+        assert inf["crt"] == 1 and inf["has_table"] == 0 and inf["table_bytes"] == 0
+        assert inf["crt_table_window"] == want, (inf, want)
+        ok(lib, lib.efl_pl_ctx_encrypt(b.h, m.data_ptr(), None, c2.data_ptr(), N, 9, 3, 1, stream()))
+        assert torch.equal(c1, c2)
+    finally:
+        a.close()
+        b.close()

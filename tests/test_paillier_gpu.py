@@ -205,6 +205,34 @@ def test_homomorphic_ops_kat(efl, k, c):
         assert kp.add(c0, c1).to_hex().strings() == [k["ops"]["add"]]
         assert kp.mul_scalar(c0, 7).to_hex().strings() == [k["ops"]["mul_scalar_7"]]
         assert kp.mul_exp2(c1, 5).to_hex().strings() == [k["ops"]["mul_exp2_5"]]
+        # every GMP-made op vector (oracle/paillier_gmp.c, paillier.cc:157-285, :722-733): both
+        # scalar signs (negative: the route through x^-1, :201-211), int64's extremes, the string
+        # overload's signed hex text, shifts 0 and 77, and the inverse
+        o = k["ops"]
+        for name, y in (("mul_scalar_0", 0), ("mul_scalar_neg", -123456789), ("mul_scalar_i64max", 2**63 - 1),
+                        ("mul_scalar_i64min", -2**63)):
+            assert kp.mul_scalar(c0, torch.tensor([y], dtype=torch.int64)).to_hex().strings() == [o[name]], name
+        assert kp.mul_scalar(c0, o["mul_scalar_hex_text"]).to_hex().strings() == [o["mul_scalar_hex"]]
+        for e in (0, 77):
+            assert kp.mul_exp2(c1, e).to_hex().strings() == [o[f"mul_exp2_{e}"]]
+        assert kp.invert(c0).to_hex().strings() == [o["invert"]]
+
+
+@pytest.mark.parametrize("k,c", fams(ALL))
+def test_matmul_gmp_kat(efl, k, c):
+    """PaillierMatmul against GMP's PaillierMatmulOp::Compute (paillier.cc:987-1035) on the KAT
+    ciphertexts: mixed-sign y with a zero and -(2^63 - 1), per-output minimum exponents."""
+    kp = keypair(efl, k)
+    mm = k["matmul"]
+    u, v, w = mm["shape"]
+    xct = efl.HexTensor.from_strings([k["vectors"][i]["c"] for i in mm["x_vectors"]], shape=(u, v))
+    xe = torch.tensor(mm["xe"], dtype=torch.int64)
+    ym = torch.tensor(mm["ym"], dtype=torch.int64)
+    ye = torch.tensor(mm["ye"], dtype=torch.int64)
+    with family(k["n_bytes"] // 4, False, c):
+        zm, ze = kp.matmul(xct, xe, ym, ye)
+    assert zm.to_hex().strings() == [h for row in mm["zm"] for h in row]
+    assert ze.cpu().tolist() == mm["ze"]
 
 
 @pytest.mark.parametrize("c", [16, 32])

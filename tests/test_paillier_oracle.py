@@ -41,6 +41,79 @@ def test_kat_restatement(k):
     assert P.decrypt(kp, int(k["ops"]["add"], 16)) == k["vectors"][5]["m"] + k["vectors"][6]["m"]
 
 
+OPS_SCALARS = {"mul_scalar_7": 7, "mul_scalar_0": 0, "mul_scalar_neg": -123456789,
+               "mul_scalar_i64max": 2**63 - 1, "mul_scalar_i64min": -2**63}
+
+
+@pytest.mark.parametrize("k", KAT["keys"], ids=lambda k: f"n{8 * k['n_bytes']}")
+def test_ops_restatement_matches_gmp_vectors(k):
+    """The GMP-computed op vectors (paillier.cc:157-285, :722-733; the signed-scalar route through
+    mpz_invert at :201-211) against the Python-int restatement, and what they decrypt to."""
+    kp = kp_of(k)
+    o = k["ops"]
+    c0, c1 = int(k["vectors"][5]["c"], 16), int(k["vectors"][6]["c"], 16)
+    m0, m1 = k["vectors"][5]["m"], k["vectors"][6]["m"]
+    for name, y in OPS_SCALARS.items():
+        assert P.hx(P.mul_scalar(kp, c0, y)) == o[name], name
+        want = m0 * y % kp.n
+        want = want - kp.n if want > kp.max_ else want
+        assert P.decrypt(kp, int(o[name], 16)) == want, name
+    assert P.hx(P.mul_scalar_hex(kp, c0, o["mul_scalar_hex_text"])) == o["mul_scalar_hex"]
+    for e in (0, 5, 77):
+        assert P.hx(P.mul_exp2(kp, c1, e)) == o[f"mul_exp2_{e}"]
+    assert P.hx(P.invert(kp, c0)) == o["invert"]
+    assert P.decrypt(kp, int(o["invert"], 16)) == -m0
+    assert P.add(kp, c0, int(o["invert"], 16)) == 1
+
+
+@pytest.mark.parametrize("k", KAT["keys"], ids=lambda k: f"n{8 * k['n_bytes']}")
+def test_matmul_restatement_matches_gmp_vectors(k):
+    """PaillierMatmul (paillier.cc:987-1035) through GMP against the Python restatement, and the
+    plaintext it decrypts to: sum_j xm*ym*2^(xe+ye-min)."""
+    kp = kp_of(k)
+    mm = k["matmul"]
+    u, v, w = mm["shape"]
+    xm = [[int(k["vectors"][mm["x_vectors"][i * v + j]]["c"], 16) for j in range(v)] for i in range(u)]
+    ms = [[k["vectors"][mm["x_vectors"][i * v + j]]["m"] for j in range(v)] for i in range(u)]
+    zm, ze = P.matmul(kp, xm, mm["xe"], mm["ym"], mm["ye"])
+    assert [[P.hx(c) for c in r] for r in zm] == mm["zm"] and ze == mm["ze"]
+    for i in range(u):
+        for q in range(w):
+            want = sum(ms[i][j] * mm["ym"][j][q] << (mm["xe"][i][j] + mm["ye"][j][q] - ze[i][q]) for j in range(v))
+            want %= kp.n
+            want = want - kp.n if want > kp.max_ else want
+            assert P.decrypt(kp, int(mm["zm"][i][q], 16)) == want
+
+
+def test_ops_gmp_live():
+    """The GMP harness reproduces the committed op and matmul vectors at test time (1024-bit key)."""
+    k = KAT["keys"][1]
+    n = int(k["n"], 16)
+    o = k["ops"]
+    c0, c1 = int(k["vectors"][5]["c"], 16), int(k["vectors"][6]["c"], 16)
+    assert P.gmp_add(n, c0, c1) == o["add"]
+    for name, y in OPS_SCALARS.items():
+        assert P.gmp_mul_scalar(n, c0, y) == o[name]
+    assert P.gmp_mul_scalar(n, c0, o["mul_scalar_hex_text"]) == o["mul_scalar_hex"]
+    assert P.gmp_mul_exp2(n, c1, 77) == o["mul_exp2_77"]
+    with pytest.raises(ValueError):
+        P.gmp_mul_exp2(n, c1, -1)
+    assert P.gmp_invert(n, c0) == o["invert"]
+    mm = k["matmul"]
+    u, v, w = mm["shape"]
+    xm = [[int(k["vectors"][mm["x_vectors"][i * v + j]]["c"], 16) for j in range(v)] for i in range(u)]
+    assert P.gmp_matmul(n, xm, mm["xe"], mm["ym"], mm["ye"]) == (mm["zm"], mm["ze"])
+
+
+def test_fbpowm_gmp_pins_every_key_size():
+    """Every KAT's hsa (2048- and 4096-bit keys included) is GMP's mpz_fbpowm through the reference's
+    table (gmp_utils.cc:56-144), recomputed live for a sample of each key."""
+    for k in KAT["keys"]:
+        kp = kp_of(k)
+        for v in k["vectors"][:2]:
+            assert P.gmp_fbpowm(kp.hs, kp.n2, k["a_bits"], v["g"], int(v["a"], 16)) == int(v["hsa"], 16)
+
+
 def test_kat_gmp_live():
     k = KAT["keys"][1]
     n, p, q = int(k["n"], 16), int(k["p"], 16), int(k["q"], 16)

@@ -5,8 +5,9 @@ views of four contiguous buffers: embedding slices of one table), batched encode
 HIP events per launch (medians over interleaved repetitions), for each of:
   plain        one table entry per slice (round 3's batched path)
   coalesced    adjacent slices merged into runs (one streaming launch when the batch is one run)
-and, for each, the fp32 batched tile shapes given in C3_SHAPES="name:enc_block,enc_k,dec_block,dec_k;..."
-(efl_fxp_tune 10-13). Prints one JSON line."""
+and, for each, the fp32 batched tile shapes given in C3_SHAPES="name:enc_block,enc_k,dec_block,dec_k
+[,enc_order,dec_order];..." (efl_fxp_tune 10-13, 17-18). C3_LAYOUTS limits the layouts (default
+"separate,views"). Prints one JSON line."""
 import json
 import os
 import sys
@@ -37,7 +38,8 @@ def main():
            torch.empty(S, 128, 128, dtype=torch.int64, device=dev),
            torch.empty(S, 128, 128, device=dev))
     views = tuple([b[i] for i in range(S)] for b in big)
-    layouts = {"separate": sep, "views": views}
+    layouts = {k: v for k, v in {"separate": sep, "views": views}.items()
+               if k in os.environ.get("C3_LAYOUTS", "separate,views").split(",")}
     tables, runs = {}, {}
     for lay, t in layouts.items():
         for co in (False, True):
@@ -55,11 +57,12 @@ def main():
         def run():
             if shape is None:
                 return fn()
-            old = [lib.efl_fxp_tune(kind, v) for kind, v in zip((10, 11, 12, 13), shape)]
+            kinds = (10, 11, 12, 13, 17, 18)[:len(shape)]
+            old = [lib.efl_fxp_tune(kind, v) for kind, v in zip(kinds, shape)]
             try:
                 return fn()
             finally:
-                for kind, v in zip((10, 11, 12, 13), old):
+                for kind, v in zip(kinds, old):
                     lib.efl_fxp_tune(kind, v)
         return run
 
@@ -90,8 +93,7 @@ def main():
             torch.cuda.synchronize()
             res[name]["encode"] += [e[0].elapsed_time(e[1]) for e in ev]
             res[name]["decode"] += [e[1].elapsed_time(e[2]) for e in ev]
-    ok = all(torch.equal(a, b) for a, b in zip(sep[0][::97], sep[3][::97])) and \
-        all(torch.equal(a, b) for a, b in zip(views[0][::97], views[3][::97]))
+    ok = all(torch.equal(a, b) for t in layouts.values() for a, b in zip(t[0][::97], t[3][::97]))
     out = {"tool": "config3_coalesce_probe", "version": efl.lib.version(), "reps": REPS * ROUNDS,
            "roundtrip_ok": ok, "runs": runs}
     for name, r in res.items():
