@@ -370,9 +370,15 @@ __global__ __launch_bounds__(kBlock) void k_scalar(typename Op::Args a, long lon
 // Batched (BASELINE config 3): tile `x` of tensor `t`, one launch for `count` tensors. Arrays of
 // pointers / sizes live in device memory (t is wave-uniform: scalar loads). Same tile shape as
 // k_stream (B lanes x K units, every load of a full tile issued before the transform).
-template <class Op, int B, int K, int NT>
+// T > 1: the workgroup walks T consecutive tiles of its tensor (xg = tile group). Round 6 PMC
+// (profiles/r06/c3_pmc*.json): per launch over the bench's 4,096 separate slices the batched kernels
+// take 90-126 k UTCL1 translation misses (and 2.6-3.4 M misses under miss) against 20-374 for the
+// streaming kernels over the same bytes in large allocations: every short workgroup pays its own
+// translation of the small fragments its 8-16 KiB of each stream sit in. A workgroup covering T
+// tiles pays it once per T tiles.
+template <class Op, int B, int K, int NT, int T = 1>
 __device__ __forceinline__ void batched_tile(const void* const* src, void* const* dst0, void* const* dst1,
-                                             const long long* ns, int flag, long long t, long long x) {
+                                             const long long* ns, int flag, long long t, long long xg) {
   // All four table entries in one scalar round trip. Left alone, the compiler loads ns[t], waits,
   // branches on it, and only then loads the three pointers: a second dependent L2 round trip at the
   // head of every workgroup, which the streaming kernel does not pay (round 6: per-launch the
@@ -390,11 +396,14 @@ __device__ __forceinline__ void batched_tile(const void* const* src, void* const
     a = DecArgs{(const long long*)sp, (const long long*)p0, p1, flag};
   }
   const long long tile = (long long)B * K * Op::kElems;
-  const long long e0 = x * tile;
-  if (e0 >= n) return;
   // 16-B alignment of this tensor's streams decides vector vs element path (uniform branch).
   const bool vec = aligned(sp, 16) && aligned(p0, 16) && aligned(p1, 16);
   const long long nunits = n / Op::kElems;
+#pragma unroll 1
+  for (int st = 0; st < T; ++st) {
+  const long long x = xg * T + st;
+  const long long e0 = x * tile;
+  if (e0 >= n) return;
   const long long u0 = x * B * K;
   if (vec) {
     typename Op::In v[K];
@@ -424,14 +433,15 @@ __device__ __forceinline__ void batched_tile(const void* const* src, void* const
   } else {
     for (long long i = e0 + threadIdx.x; i < n && i < e0 + tile; i += B) Op::scalar(a, i);
   }
+  }
 }
 
-// 2-D grid: blockIdx.y = tensor (from tile_base), blockIdx.x = tile of that tensor.
-template <class Op, int B, int K, int NT>
+// 2-D grid: blockIdx.y = tensor (from tile_base), blockIdx.x = group of T tiles of that tensor.
+template <class Op, int B, int K, int NT, int T = 1>
 __global__ __launch_bounds__(B) void k_batched(const void* const* src, void* const* dst0,
                                                void* const* dst1, const long long* ns,
                                                int flag, long long tile_base) {
-  batched_tile<Op, B, K, NT>(src, dst0, dst1, ns, flag, tile_base + blockIdx.y, blockIdx.x);
+  batched_tile<Op, B, K, NT, T>(src, dst0, dst1, ns, flag, tile_base + blockIdx.y, blockIdx.x);
 }
 
 // 1-D grid over count x gx tiles (tensor-major), XCD-aware like k_stream: workgroups are dispatched
@@ -601,6 +611,9 @@ std::atomic<int> g_batch_k[2] = {{1}, {2}};
 // efl_fxp_tune 17 / 18: tile order of the fp32 batched encode / decode: 0 2-D grid (tensor =
 // blockIdx.y), 1 one flat tensor-major grid, 2 the flat grid in XCD-aware order
 std::atomic<int> g_batch_order[2] = {{0}, {0}};
+// efl_fxp_tune 26 / 27: tiles per workgroup of the fp32 batched encode / decode (2-D grid, 512-lane
+// tiles; 1, 2, 4, 8): fewer, longer workgroups, each translating its tensor's pages once
+std::atomic<int> g_batch_tiles[2] = {{1}, {1}};
 // efl_fxp_tune 19: workgroups of the persistent batched walk (order 3)
 std::atomic<int> g_batch_persist_grid{2048};
 // The fp64 encode (8 B read, 16 B written per element) through its own shape: efl_fxp_tune kinds
@@ -733,6 +746,14 @@ namespace efl {
 // efl_fxp_tune(20, nb): Philox blocks per lane of the DP noise kernel (csrc/mask.hip; 1, 2, 4). 4:
 // 0.669 / 0.685 of 8 TB/s against 0.594 / 0.366 for one block on two boxes (profiles/r03/bench_mask*)
 std::atomic<int> g_dp_blocks{4};
+// efl_fxp_tune(25, nb) / (28, st): lane groups (Philox blocks) per lane (1, 2, 4) and store flavour
+// (0 plain, 2 nontemporal, 7 `nt sc1`) of the secret-sharing mask kernels, per family [noise (op 0),
+// share / weight noise (ops 1, 2), mask_cols, mask_rows]; setting a kind sets all four. Defaults:
+// the best of the round-6 sweep on three boxes (tools/bench_mask.py, profiles/r06/bench_mask*.jsonl):
+// noise 2 / plain 0.87-0.90, share 1 / nt sc1 0.71-0.78, mask_cols 1 / nt 0.89, mask_rows 1 / nt sc1
+// 0.67
+std::atomic<int> g_mask_blocks[4] = {{2}, {1}, {1}, {1}};
+std::atomic<int> g_mask_store[4] = {{0}, {7}, {2}, {7}};
 }  // namespace efl
 
 EFL_API int efl_fxp_tune(int kind, int value) {
@@ -752,7 +773,22 @@ EFL_API int efl_fxp_tune(int kind, int value) {
         return g_xcd64.exchange(value);
     }
   }
+  if (kind == 25 || kind == 28) {   // mask kernels: lane groups per lane / store flavour, every family
+    std::atomic<int>* v = kind == 25 ? g_mask_blocks : g_mask_store;
+    if (value == -1) return v[0].load();
+    if (value == -2) {              // back to the per-family defaults
+      static const int kDef[2][4] = {{2, 1, 1, 1}, {0, 7, 2, 7}};
+      for (int f = 0; f < 4; ++f) v[f].store(kDef[kind == 25 ? 0 : 1][f]);
+      return 0;
+    }
+    if (kind == 25 && value != 1 && value != 2 && value != 4) return EFL_E_INVALID_ARGUMENT;
+    if (kind == 28 && value != 0 && value != 2 && value != 7) return EFL_E_INVALID_ARGUMENT;
+    const int prev = v[0].load();
+    for (int f = 0; f < 4; ++f) v[f].store(value);
+    return prev;
+  }
   if (kind == 20) {                 // DP noise kernel: Philox blocks per lane (csrc/mask.hip)
+    if (value == -1) return g_dp_blocks.load();
     if (value != 1 && value != 2 && value != 4) return EFL_E_INVALID_ARGUMENT;
     return g_dp_blocks.exchange(value);
   }
@@ -763,6 +799,12 @@ EFL_API int efl_fxp_tune(int kind, int value) {
   if (kind == 16) {                 // streaming fp32 encode: exponent stores first
     if (value != 0 && value != 1) return EFL_E_INVALID_ARGUMENT;
     return g_e_first.exchange(value);
+  }
+  if (kind == 26 || kind == 27) {   // batched fp32 encode / decode: tiles per workgroup
+    std::atomic<int>& v = g_batch_tiles[kind - 26];
+    if (value == -1) return v.load();
+    if (value != 1 && value != 2 && value != 4 && value != 8) return EFL_E_INVALID_ARGUMENT;
+    return v.exchange(value);
   }
   if (kind == 19) {                 // persistent batched walk: workgroups
     if (value < 1) return EFL_E_INVALID_ARGUMENT;
@@ -914,10 +956,21 @@ hipError_t launch_batched_bk(const void* const* src, void* const* d0, void* cons
                        gx, total, per);
     return hipGetLastError();
   }
+  const int T = (dir >= 0 && B == 512) ? g_batch_tiles[dir].load(std::memory_order_relaxed) : 1;
+  const long long gxt = (gx + T - 1) / T;
   for (long long b = 0; b < count; b += kMaxGridY) {
     const long long gy = count - b < kMaxGridY ? count - b : kMaxGridY;
-    hipLaunchKernelGGL((k_batched<Op, B, K, NT>), dim3((unsigned)gx, (unsigned)gy), dim3(B), 0, s,
-                       src, d0, d1, ns, flag, b);
+    const dim3 grid((unsigned)gxt, (unsigned)gy);
+    if constexpr (B == 512) {
+      switch (T) {
+        case 2: hipLaunchKernelGGL((k_batched<Op, B, K, NT, 2>), grid, dim3(B), 0, s, src, d0, d1, ns, flag, b); break;
+        case 4: hipLaunchKernelGGL((k_batched<Op, B, K, NT, 4>), grid, dim3(B), 0, s, src, d0, d1, ns, flag, b); break;
+        case 8: hipLaunchKernelGGL((k_batched<Op, B, K, NT, 8>), grid, dim3(B), 0, s, src, d0, d1, ns, flag, b); break;
+        default: hipLaunchKernelGGL((k_batched<Op, B, K, NT>), grid, dim3(B), 0, s, src, d0, d1, ns, flag, b); break;
+      }
+    } else {
+      hipLaunchKernelGGL((k_batched<Op, B, K, NT>), grid, dim3(B), 0, s, src, d0, d1, ns, flag, b);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

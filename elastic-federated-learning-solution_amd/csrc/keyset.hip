@@ -714,20 +714,32 @@ int ensure_crt(efl_pl_ctx* c, hipStream_t s, bool* ok) {
     c->crt = -1;
     return EFL_OK;
   }
-  // A key that got its public half first (set_public, then set_private: the reference's usual order)
-  // built the n^2 table the owner's CRT encryption does not walk: it is released, so the sub-tables
-  // are sized against the whole budget as with efl_pl_set_keypair (W 18 -> 12 otherwise).
-  // An explicit window keeps it (the caller sized the tables).
-  if (c->main->has_table && !c->window) {
-    KS_RC(drop_table(*c->main, s));
-    ++c->generation;
-  }
   // the two sub-tables take half each of what the context may hold (round 4's split: W = 18 for the
   // examples' 1024-bit key under the 4 GiB default); the owner's own n^2 table, built only if the
   // public-key path is walked, is sized against what the budget has left then
-  const int64_t each = c->allowance() / 2;
+  int64_t each = c->allowance() / 2;
   std::unique_ptr<Block> sb[2];
   for (int i = 0; i < 2; ++i) {
+    if (i == 0 && c->main->has_table && !c->window) {
+      // A key that got its public half first (set_public, then set_private: the reference's usual
+      // order) holds the n^2 table the owner's CRT encryption does not walk. When keeping it would
+      // give the sub-tables a narrower window than releasing it (W 18 -> 12 under the
+      // 4 GiB default), it is released and the sub-tables are sized as efl_pl_set_keypair sizes
+      // them; with room for both (a larger budget) it stays. An explicit window keeps it too.
+      Block probe;
+      const Big R0 = hb::mul(R, ip);
+      int rc = plan_block(probe, m.p, hb::mod(m.hs, p2), m.a_bits, m.g, nullptr, nullptr, 0, each, &R0);
+      if ((rc == EFL_OK || rc == EFL_E_RESOURCE_EXHAUSTED) && probe.lc > 0) {
+        const int64_t freed = std::max<int64_t>(0, std::min(c->cap_bytes(), budget_left() + c->main->table_bytes)) / 2;
+        const int w_keep = rc == EFL_OK ? probe.W : 0;
+        const int w_drop = choose_window(m.a_bits, 4LL * (probe.lc + probe.L28), freed);
+        if (w_drop > w_keep) {
+          KS_RC(drop_table(*c->main, s));
+          ++c->generation;
+          each = c->allowance() / 2;
+        }
+      }
+    }
     const Big& x = i ? m.q : m.p;
     const Big x2 = i ? q2 : p2;
     const Big start = hb::mul(R, i ? iq : ip);    // walks give hs^(a') R (q^2)^-1 mod p^2, ...

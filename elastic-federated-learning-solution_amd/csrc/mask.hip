@@ -35,14 +35,26 @@ namespace {
 
 using pl::philox;
 
-// EFL_MASK_NT=1 builds nontemporal stores (tuning variant; the default is chosen by measurement)
-#ifndef EFL_MASK_NT
-#define EFL_MASK_NT 0
-#endif
-template <class T>
+// Store flavour of the mask kernels (efl_fxp_tune kind 28): 0 plain stores, 2 nontemporal (`nt`),
+// 7 `global_store_dwordx{2,4} ... nt sc1` (the line leaves the XCD's L2 as it is written; the
+// streaming encode's flavour). The DP kernel keeps plain stores.
+typedef int i4m __attribute__((ext_vector_type(4)));
+typedef int i2m __attribute__((ext_vector_type(2)));
+template <int ST = 0, class T>
 __device__ __forceinline__ void stv(T* p, T v) {
-  if constexpr (EFL_MASK_NT) __builtin_nontemporal_store(v, p);
-  else *p = v;
+  if constexpr (ST == 7 && sizeof(T) == 16) {
+    const i4m w = __builtin_bit_cast(i4m, v);
+    // a VALU write to the data VGPRs right after a >8-byte store needs a wait state the hazard
+    // recognizer cannot see inside asm (tests/test_isa_guard.py checks the s_nop)
+    asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" ::"v"(p), "v"(w) : "memory");
+  } else if constexpr (ST == 7 && sizeof(T) == 8) {
+    const i2m w = __builtin_bit_cast(i2m, v);
+    asm volatile("global_store_dwordx2 %0, %1, off nt sc1\n\ts_nop 1" ::"v"(p), "v"(w) : "memory");
+  } else if constexpr (ST == 2) {
+    __builtin_nontemporal_store(v, p);
+  } else {
+    *p = v;
+  }
 }
 
 __device__ __forceinline__ float u01(uint32_t w) {
@@ -56,60 +68,119 @@ __device__ __forceinline__ void draw4(uint64_t seed, uint64_t blk, float (&u)[4]
   for (int j = 0; j < 4; ++j) u[j] = u01(c[j]);
 }
 
-// noise n = U * x (then / d when d != 1, as `noise / noise_divisor` in the reference)
-__device__ __forceinline__ float noise(float u, float x, float d, bool div) {
+// noise n = U * x (then / d when d != 1, as `noise / noise_divisor` in the reference). DIV is a
+// template parameter (0 none, 1 times the exact reciprocal of a power-of-two d — the same rounding
+// as the division — 2 the IEEE division): as a runtime flag the compiler computed the division for
+// every element and selected (about 11 VALU instructions each, round 6 ISA).
+template <int DIV>
+__device__ __forceinline__ float noise(float u, float x, float d) {
   const float n = u * x;
-  return div ? n / d : n;
+  if constexpr (DIV == 1) return n * d;
+  else if constexpr (DIV == 2) return n / d;
+  else return n;
+}
+
+// Division of a lane-group index by the row length: q = g / d for g < 2^31 as one 64-bit product and
+// a shift (Granlund-Montgomery: l = ceil(log2 d), m = floor(2^(31 + l) / d) + 1 < 2^32 is exact for
+// every g < 2^31), from the magic (m, 31 + l) the host passes; m == 0 (more than 2^31 groups) takes
+// the 64-bit division.
+__device__ __forceinline__ long long div_groups(long long g, long long d, uint32_t m, int sh) {
+  if (m) return (long long)(((uint64_t)(uint32_t)g * m) >> sh);
+  return g / d;
 }
 
 // op 0: o0 = n            (generate_suitable_noise)
 // op 1: o0 = n, o1 = x-n  (share: the sent share and the kept one)
 // op 2: o0 = x-n, o1 = x+n (Dense weight noise: sent and kept)
-template <int OP>
+// One lane owns NB Philox blocks (4 elements each) kBlock lanes apart, so a wave's accesses stay
+// 64 x 16 contiguous bytes; the loads of all NB blocks are issued first and the NB Philox chains
+// run round by round together while they travel (round 6, the DP kernel's round-5 structure: one
+// block per lane drew the uniforms before loading x, with nothing in flight meanwhile).
+template <int OP, int DIV>
+__device__ __forceinline__ void noise_f4(const f4& v, const float (&u)[4], float d, f4& a, f4& b) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float nz = noise<DIV>(u[j], v[j], d);
+    if (OP == 0) a[j] = nz;
+    if (OP == 1) { a[j] = nz; b[j] = v[j] - nz; }
+    if (OP == 2) { a[j] = v[j] - nz; b[j] = v[j] + nz; }
+  }
+}
+
+template <int NB>
+__device__ __forceinline__ void uniforms(uint64_t seed, const uint64_t (&blk)[NB], float (&u)[NB][4]) {
+  uint32_t c[NB][4];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    c[b][0] = (uint32_t)blk[b];
+    c[b][1] = (uint32_t)(blk[b] >> 32);
+    c[b][2] = 0u;
+    c[b][3] = 0u;
+  }
+  pl::philox_n<NB>(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) u[b][j] = u01(c[b][j]);
+}
+
+template <int OP, int DIV, int NB, int ST>
 __global__ __launch_bounds__(kBlock) void k_noise(const float* __restrict__ x, float* __restrict__ o0,
                                                   float* __restrict__ o1, long long n, uint64_t seed,
-                                                  uint64_t ctr0, float d, int div) {
-  const long long g = (long long)blockIdx.x * kBlock + threadIdx.x;
-  const long long i0 = g * 4;
-  if (i0 >= n) return;
-  float u[4];
-  draw4(seed, ctr0 + (uint64_t)g, u);
-  if (i0 + 4 <= n) {
-    const f4 v = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + g);
-    f4 a, b;
+                                                  uint64_t ctr0, float d) {
+  const long long g0 = (long long)blockIdx.x * (kBlock * NB) + threadIdx.x;
+  if (g0 * 4 >= n) return;
+  if ((g0 + (long long)(NB - 1) * kBlock) * 4 + 4 <= n) {
+    f4 v[NB];
+    uint64_t blk[NB];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float nz = noise(u[j], v[j], d, div);
-      if (OP == 0) a[j] = nz;
-      if (OP == 1) { a[j] = nz; b[j] = v[j] - nz; }
-      if (OP == 2) { a[j] = v[j] - nz; b[j] = v[j] + nz; }
+    for (int b = 0; b < NB; ++b) {
+      v[b] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + g0 + b * kBlock);
+      blk[b] = ctr0 + (uint64_t)(g0 + b * kBlock);
     }
-    stv(reinterpret_cast<f4*>(o0) + g, a);
-    if (OP != 0) stv(reinterpret_cast<f4*>(o1) + g, b);
-  } else {
-    for (int j = 0; j < 4 && i0 + j < n; ++j) {
-      const float xv = x[i0 + j];
-      const float nz = noise(u[j], xv, d, div);
-      if (OP == 0) o0[i0 + j] = nz;
-      if (OP == 1) { o0[i0 + j] = nz; o1[i0 + j] = xv - nz; }
-      if (OP == 2) { o0[i0 + j] = xv - nz; o1[i0 + j] = xv + nz; }
+    float u[NB][4];
+    uniforms<NB>(seed, blk, u);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      f4 a, c;
+      noise_f4<OP, DIV>(v[b], u[b], d, a, c);
+      stv<ST>(reinterpret_cast<f4*>(o0) + g0 + b * kBlock, a);
+      if (OP != 0) stv<ST>(reinterpret_cast<f4*>(o1) + g0 + b * kBlock, c);
+    }
+    return;
+  }
+  for (int b = 0; b < NB; ++b) {
+    const long long g = g0 + b * kBlock, i0 = g * 4;
+    if (i0 >= n) break;
+    float u[4];
+    draw4(seed, ctr0 + (uint64_t)g, u);
+    if (i0 + 4 <= n) {
+      const f4 v = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + g);
+      f4 a, c;
+      noise_f4<OP, DIV>(v, u, d, a, c);
+      stv<ST>(reinterpret_cast<f4*>(o0) + g, a);
+      if (OP != 0) stv<ST>(reinterpret_cast<f4*>(o1) + g, c);
+    } else {
+      for (int j = 0; j < 4 && i0 + j < n; ++j) {
+        const float xv = x[i0 + j];
+        const float nz = noise<DIV>(u[j], xv, d);
+        if (OP == 0) o0[i0 + j] = nz;
+        if (OP == 1) { o0[i0 + j] = nz; o1[i0 + j] = xv - nz; }
+        if (OP == 2) { o0[i0 + j] = xv - nz; o1[i0 + j] = xv + nz; }
+      }
     }
   }
 }
 
 // Mode A, a [R, C] with C % 8 == 0 (every row of send, width 3C/2, then starts 16-byte aligned):
-// lane g owns a[r, 4q .. 4q+3] (element index 4g).
+// lane group g owns a[r, 4q .. 4q+3] (element index 4g); a lane owns NB groups kBlock apart, loads
+// first, Philox chains together (as k_noise).
 // send [R, 3C/2] = [a + e | e_even + e_odd], keep0 [R, C] = a - e, keep1 [R, C/2] = e_odd - e_even.
-__global__ __launch_bounds__(kBlock) void k_mask_cols4(const float* __restrict__ a, float* __restrict__ send,
-                                                       float* __restrict__ keep0, float* __restrict__ keep1,
-                                                       long long R, long long C, uint64_t seed, uint64_t ctr0) {
-  const long long g = (long long)blockIdx.x * kBlock + threadIdx.x;
-  const long long q4 = C / 4;
-  if (g >= R * q4) return;
-  const long long r = g / q4, q = g - r * q4;
-  float u[4];
-  draw4(seed, ctr0 + (uint64_t)g, u);
-  const f4 v = __builtin_nontemporal_load(reinterpret_cast<const f4*>(a) + g);
+template <int ST>
+__device__ __forceinline__ void mask_cols_store(const f4& v, const float (&u)[4], long long g, long long q4,
+                                                long long C, float* __restrict__ send, float* __restrict__ keep0,
+                                                float* __restrict__ keep1, uint32_t dm, int ds) {
+  const long long r = div_groups(g, q4, dm, ds), q = g - r * q4;
   f4 s, k;
   float e[4];
 #pragma unroll
@@ -119,15 +190,47 @@ __global__ __launch_bounds__(kBlock) void k_mask_cols4(const float* __restrict__
     k[j] = v[j] - e[j];
   }
   const long long W = C + C / 2;
-  stv(reinterpret_cast<f4*>(send + r * W + 4 * q), s);
-  stv(reinterpret_cast<f4*>(keep0) + g, k);
+  stv<ST>(reinterpret_cast<f4*>(send + r * W + 4 * q), s);
+  stv<ST>(reinterpret_cast<f4*>(keep0) + g, k);
   f2 p, m;
   p[0] = e[0] + e[1];
   p[1] = e[2] + e[3];
   m[0] = e[1] - e[0];
   m[1] = e[3] - e[2];
-  stv(reinterpret_cast<f2*>(send + r * W + C + 2 * q), p);
-  stv(reinterpret_cast<f2*>(keep1 + r * (C / 2) + 2 * q), m);
+  stv<ST>(reinterpret_cast<f2*>(send + r * W + C + 2 * q), p);
+  stv<ST>(reinterpret_cast<f2*>(keep1 + r * (C / 2) + 2 * q), m);
+}
+
+template <int NB, int ST>
+__global__ __launch_bounds__(kBlock) void k_mask_cols4(const float* __restrict__ a, float* __restrict__ send,
+                                                       float* __restrict__ keep0, float* __restrict__ keep1,
+                                                       long long R, long long C, uint64_t seed, uint64_t ctr0,
+                                                       uint32_t dm, int ds) {
+  const long long g0 = (long long)blockIdx.x * (kBlock * NB) + threadIdx.x;
+  const long long q4 = C / 4, total = R * q4;
+  if (g0 >= total) return;
+  if (g0 + (long long)(NB - 1) * kBlock < total) {
+    f4 v[NB];
+    uint64_t blk[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      v[b] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(a) + g0 + b * kBlock);
+      blk[b] = ctr0 + (uint64_t)(g0 + b * kBlock);
+    }
+    float u[NB][4];
+    uniforms<NB>(seed, blk, u);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) mask_cols_store<ST>(v[b], u[b], g0 + b * kBlock, q4, C, send, keep0, keep1, dm, ds);
+    return;
+  }
+  for (int b = 0; b < NB; ++b) {
+    const long long g = g0 + b * kBlock;
+    if (g >= total) break;
+    float u[4];
+    draw4(seed, ctr0 + (uint64_t)g, u);
+    mask_cols_store<ST>(__builtin_nontemporal_load(reinterpret_cast<const f4*>(a) + g), u, g, q4, C, send, keep0, keep1,
+                        dm, ds);
+  }
 }
 
 // Mode A for other even C: one lane per column pair (2 elements), Philox word chosen per element.
@@ -153,31 +256,14 @@ __global__ __launch_bounds__(kBlock) void k_mask_cols2(const float* __restrict__
   keep1[r * h + j] = e1 - e0;
 }
 
-// Mode B, b [K, N] with K even: lane g owns columns 4q..4q+3 of rows 2j and 2j+1 (N % 4 == 0) or
-// one column (general N). Element index of b[r, c] is r*N + c.
+// Mode B, b [K, N] with K even: lane group g owns columns 4q..4q+3 of rows 2j and 2j+1 (N % 4 == 0)
+// or one column (general N). Element index of b[r, c] is r*N + c.
 // send [3K/2, N] = [b/2 - f ; f_even - f_odd], keep0 [K, N] = b/2 + f, keep1 [K/2, N] = f_odd + f_even.
-template <int V>
-__global__ __launch_bounds__(kBlock) void k_mask_rows(const float* __restrict__ b, float* __restrict__ send,
-                                                      float* __restrict__ keep0, float* __restrict__ keep1,
-                                                      long long K, long long N, uint64_t seed, uint64_t ctr0) {
-  const long long g = (long long)blockIdx.x * kBlock + threadIdx.x;
-  const long long nq = N / V;
-  if (g >= (K / 2) * nq) return;
-  const long long j = g / nq, q = g - j * nq;
-  const long long ie = 2 * j * N + V * q, io = ie + N;   // a[2j, Vq], a[2j+1, Vq]
-  float ue[4], uo[4];
-  draw4(seed, ctr0 + (uint64_t)(ie >> 2), ue);
-  draw4(seed, ctr0 + (uint64_t)(io >> 2), uo);
-  float xe[V], xo[V];
-  if (V == 4) {
-    const f4 ve = __builtin_nontemporal_load(reinterpret_cast<const f4*>(b + ie));
-    const f4 vo = __builtin_nontemporal_load(reinterpret_cast<const f4*>(b + io));
-#pragma unroll
-    for (int t = 0; t < V; ++t) { xe[t] = ve[t]; xo[t] = vo[t]; }
-  } else {
-    xe[0] = b[ie];
-    xo[0] = b[io];
-  }
+template <int V, int ST>
+__device__ __forceinline__ void mask_rows_store(const float (&xe)[V], const float (&xo)[V], const float (&ue)[4],
+                                                const float (&uo)[4], long long ie, long long io, long long idf,
+                                                long long ik, float* __restrict__ send, float* __restrict__ keep0,
+                                                float* __restrict__ keep1) {
   float se[V], so[V], ke[V], ko[V], sd[V], kd[V];
 #pragma unroll
   for (int t = 0; t < V; ++t) {
@@ -191,15 +277,13 @@ __global__ __launch_bounds__(kBlock) void k_mask_rows(const float* __restrict__ 
     sd[t] = fe - fo;
     kd[t] = fo + fe;
   }
-  const long long idf = K * N + j * N + V * q;   // row K + j of send
-  const long long ik = j * N + V * q;            // row j of keep1
   if (V == 4) {
-    stv(reinterpret_cast<f4*>(send + ie), f4{se[0], se[1], se[2], se[3]});
-    stv(reinterpret_cast<f4*>(send + io), f4{so[0], so[1], so[2], so[3]});
-    stv(reinterpret_cast<f4*>(keep0 + ie), f4{ke[0], ke[1], ke[2], ke[3]});
-    stv(reinterpret_cast<f4*>(keep0 + io), f4{ko[0], ko[1], ko[2], ko[3]});
-    stv(reinterpret_cast<f4*>(send + idf), f4{sd[0], sd[1], sd[2], sd[3]});
-    stv(reinterpret_cast<f4*>(keep1 + ik), f4{kd[0], kd[1], kd[2], kd[3]});
+    stv<ST>(reinterpret_cast<f4*>(send + ie), f4{se[0], se[1], se[2], se[3]});
+    stv<ST>(reinterpret_cast<f4*>(send + io), f4{so[0], so[1], so[2], so[3]});
+    stv<ST>(reinterpret_cast<f4*>(keep0 + ie), f4{ke[0], ke[1], ke[2], ke[3]});
+    stv<ST>(reinterpret_cast<f4*>(keep0 + io), f4{ko[0], ko[1], ko[2], ko[3]});
+    stv<ST>(reinterpret_cast<f4*>(send + idf), f4{sd[0], sd[1], sd[2], sd[3]});
+    stv<ST>(reinterpret_cast<f4*>(keep1 + ik), f4{kd[0], kd[1], kd[2], kd[3]});
   } else {
     send[ie] = se[0];
     send[io] = so[0];
@@ -207,6 +291,69 @@ __global__ __launch_bounds__(kBlock) void k_mask_rows(const float* __restrict__ 
     keep0[io] = ko[0];
     send[idf] = sd[0];
     keep1[ik] = kd[0];
+  }
+}
+
+// V = 4: a lane owns NB groups kBlock apart (2 NB Philox blocks), loads first, chains together
+template <int V, int NB, int ST>
+__global__ __launch_bounds__(kBlock) void k_mask_rows(const float* __restrict__ b, float* __restrict__ send,
+                                                      float* __restrict__ keep0, float* __restrict__ keep1,
+                                                      long long K, long long N, uint64_t seed, uint64_t ctr0,
+                                                      uint32_t dm, int ds) {
+  const long long g0 = (long long)blockIdx.x * (kBlock * NB) + threadIdx.x;
+  const long long nq = N / V, total = (K / 2) * nq;
+  if (g0 >= total) return;
+  if (V == 4 && g0 + (long long)(NB - 1) * kBlock < total) {
+    long long ie[NB], io[NB];
+    f4 ve[NB], vo[NB];
+    uint64_t blk[2 * NB];
+#pragma unroll
+    for (int t = 0; t < NB; ++t) {
+      const long long g = g0 + t * kBlock;
+      const long long j = div_groups(g, nq, dm, ds), q = g - j * nq;
+      ie[t] = 2 * j * N + V * q;
+      io[t] = ie[t] + N;
+      ve[t] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(b + ie[t]));
+      vo[t] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(b + io[t]));
+      blk[2 * t] = ctr0 + (uint64_t)(ie[t] >> 2);
+      blk[2 * t + 1] = ctr0 + (uint64_t)(io[t] >> 2);
+    }
+    float u[2 * NB][4];
+    uniforms<2 * NB>(seed, blk, u);
+#pragma unroll
+    for (int t = 0; t < NB; ++t) {
+      const long long g = g0 + t * kBlock;
+      const long long j = div_groups(g, nq, dm, ds), q = g - j * nq;
+      float xe[V], xo[V];
+#pragma unroll
+      for (int c = 0; c < V; ++c) {
+        xe[c] = ve[t][c];
+        xo[c] = vo[t][c];
+      }
+      mask_rows_store<V, ST>(xe, xo, u[2 * t], u[2 * t + 1], ie[t], io[t], K * N + j * N + V * q, j * N + V * q, send,
+                         keep0, keep1);
+    }
+    return;
+  }
+  for (int t = 0; t < NB; ++t) {
+    const long long g = g0 + t * kBlock;
+    if (g >= total) break;
+    const long long j = div_groups(g, nq, dm, ds), q = g - j * nq;
+    const long long ie = 2 * j * N + V * q, io = ie + N;   // a[2j, Vq], a[2j+1, Vq]
+    float ue[4], uo[4];
+    draw4(seed, ctr0 + (uint64_t)(ie >> 2), ue);
+    draw4(seed, ctr0 + (uint64_t)(io >> 2), uo);
+    float xe[V], xo[V];
+    if (V == 4) {
+      const f4 a = __builtin_nontemporal_load(reinterpret_cast<const f4*>(b + ie));
+      const f4 c = __builtin_nontemporal_load(reinterpret_cast<const f4*>(b + io));
+#pragma unroll
+      for (int k = 0; k < V; ++k) { xe[k] = a[k]; xo[k] = c[k]; }
+    } else {
+      xe[0] = b[ie];
+      xo[0] = b[io];
+    }
+    mask_rows_store<V, ST>(xe, xo, ue, uo, ie, io, K * N + j * N + V * q, j * N + V * q, send, keep0, keep1);
   }
 }
 
@@ -341,10 +488,53 @@ void launch_dp(int nb, long long lanes, const float* x, float* o, long long n, u
 
 bool lanes_ok(long long lanes) { return lanes / kBlock < (1ll << 31); }
 
+// one launch of a mask kernel at nb lane groups per lane (1, 2, 4) and store flavour st (0, 2, 7):
+// KERNEL(NB, ST) names the instance
+#define EFL_MASK_LAUNCH(nb, st, lanes, s, KERNEL, ...)                                                \
+  do {                                                                                               \
+    const unsigned g1_ = grid_for(lanes);                                                            \
+    const int nb_ = (nb), st_ = (st);                                                                \
+    const unsigned gr_ = nb_ == 4 ? (g1_ + 3) / 4 : nb_ == 2 ? (g1_ + 1) / 2 : g1_;                  \
+    if (nb_ == 4 && st_ == 7) KERNEL(4, 7)<<<gr_, kBlock, 0, s>>>(__VA_ARGS__);                      \
+    else if (nb_ == 4 && st_ == 2) KERNEL(4, 2)<<<gr_, kBlock, 0, s>>>(__VA_ARGS__);                 \
+    else if (nb_ == 4) KERNEL(4, 0)<<<gr_, kBlock, 0, s>>>(__VA_ARGS__);                             \
+    else if (nb_ == 2 && st_ == 7) KERNEL(2, 7)<<<gr_, kBlock, 0, s>>>(__VA_ARGS__);                 \
+    else if (nb_ == 2 && st_ == 2) KERNEL(2, 2)<<<gr_, kBlock, 0, s>>>(__VA_ARGS__);                 \
+    else if (nb_ == 2) KERNEL(2, 0)<<<gr_, kBlock, 0, s>>>(__VA_ARGS__);                             \
+    else if (st_ == 7) KERNEL(1, 7)<<<gr_, kBlock, 0, s>>>(__VA_ARGS__);                             \
+    else if (st_ == 2) KERNEL(1, 2)<<<gr_, kBlock, 0, s>>>(__VA_ARGS__);                             \
+    else KERNEL(1, 0)<<<gr_, kBlock, 0, s>>>(__VA_ARGS__);                                           \
+  } while (0)
+#define EFL_K_NOISE0D0(NB, ST) k_noise<0, 0, NB, ST>
+#define EFL_K_NOISE0D1(NB, ST) k_noise<0, 1, NB, ST>
+#define EFL_K_NOISE0D2(NB, ST) k_noise<0, 2, NB, ST>
+#define EFL_K_NOISE1D0(NB, ST) k_noise<1, 0, NB, ST>
+#define EFL_K_NOISE1D1(NB, ST) k_noise<1, 1, NB, ST>
+#define EFL_K_NOISE1D2(NB, ST) k_noise<1, 2, NB, ST>
+#define EFL_K_NOISE2D0(NB, ST) k_noise<2, 0, NB, ST>
+#define EFL_K_NOISE2D1(NB, ST) k_noise<2, 1, NB, ST>
+#define EFL_K_NOISE2D2(NB, ST) k_noise<2, 2, NB, ST>
+
+// the magic (m, shift) of div_groups for d, or m = 0 when the groups pass 2^31
+void group_magic(long long total, long long d, uint32_t* m, int* sh) {
+  *m = 0;
+  *sh = 0;
+  if (total <= 0 || total >= (1ll << 31) || d <= 0) return;
+  int l = 0;
+  while ((1ll << l) < d) ++l;
+  *m = (uint32_t)(((1ull << (31 + l)) / (unsigned long long)d) + 1ull);
+  *sh = 31 + l;
+}
+#define EFL_K_COLS4(NB, ST) k_mask_cols4<NB, ST>
+#define EFL_K_ROWS4(NB, ST) k_mask_rows<4, NB, ST>
+
 }  // namespace
 
-// efl_fxp_tune(20, nb): Philox blocks per lane of the DP noise kernel (defined in fxp.hip)
+// efl_fxp_tune(20, nb): Philox blocks per lane of the DP noise kernel (defined in fxp.hip);
+// efl_fxp_tune(25, nb) / (28, st): lane groups per lane / store flavour of the mask kernels
 extern std::atomic<int> g_dp_blocks;
+extern std::atomic<int> g_mask_blocks[4];   // [noise, share / weight noise, mask_cols, mask_rows]
+extern std::atomic<int> g_mask_store[4];
 
 }  // namespace efl
 
@@ -364,12 +554,29 @@ EFL_API int efl_ss_noise(const float* x, float* out0, float* out1, int64_t n, in
   const long long lanes = (n + 3) / 4;
   if (!lanes_ok(lanes)) { set_error("efl_ss_noise: tensor too large"); return EFL_E_INVALID_ARGUMENT; }
   hipStream_t s = (hipStream_t)stream;
-  const int div = divisor != 1.0f;
-  switch (op) {
-    case 0: k_noise<0><<<grid_for(lanes), kBlock, 0, s>>>(x, out0, out1, n, seed, ctr0, divisor, div); break;
-    case 1: k_noise<1><<<grid_for(lanes), kBlock, 0, s>>>(x, out0, out1, n, seed, ctr0, divisor, div); break;
-    default: k_noise<2><<<grid_for(lanes), kBlock, 0, s>>>(x, out0, out1, n, seed, ctr0, divisor, div); break;
+  // divisor 1: no division; a power of two with a normal reciprocal: times the reciprocal (the same
+  // correctly rounded value); otherwise the division
+  int ex = 0;
+  const bool pow2 = std::isfinite(divisor) && std::frexp(std::fabs(divisor), &ex) == 0.5f &&
+                    std::isnormal(1.0f / divisor);
+  const int dv = divisor == 1.0f ? 0 : pow2 ? 1 : 2;
+  const float d = dv == 1 ? 1.0f / divisor : divisor;
+  const int fam = op == 0 ? 0 : 1;
+  const int nb = g_mask_blocks[fam].load(std::memory_order_relaxed);
+  const int st = g_mask_store[fam].load(std::memory_order_relaxed);
+#define EFL_NOISE_OP(OPD) EFL_MASK_LAUNCH(nb, st, lanes, s, OPD, x, out0, out1, n, seed, ctr0, d)
+  switch (op * 3 + dv) {
+    case 0: EFL_NOISE_OP(EFL_K_NOISE0D0); break;
+    case 1: EFL_NOISE_OP(EFL_K_NOISE0D1); break;
+    case 2: EFL_NOISE_OP(EFL_K_NOISE0D2); break;
+    case 3: EFL_NOISE_OP(EFL_K_NOISE1D0); break;
+    case 4: EFL_NOISE_OP(EFL_K_NOISE1D1); break;
+    case 5: EFL_NOISE_OP(EFL_K_NOISE1D2); break;
+    case 6: EFL_NOISE_OP(EFL_K_NOISE2D0); break;
+    case 7: EFL_NOISE_OP(EFL_K_NOISE2D1); break;
+    default: EFL_NOISE_OP(EFL_K_NOISE2D2); break;
   }
+#undef EFL_NOISE_OP
   return hip_status(hipGetLastError(), "efl_ss_noise");
 }
 
@@ -385,7 +592,13 @@ EFL_API int efl_ss_mask_cols(const float* a, float* send, float* keep0, float* k
   const bool v4 = cols % 8 == 0 && aligned(a, 16) && aligned(send, 16) && aligned(keep0, 16) && aligned(keep1, 8);
   const long long lanes = v4 ? rows * (cols / 4) : rows * (cols / 2);
   if (!lanes_ok(lanes)) { set_error("efl_ss_mask_cols: tensor too large"); return EFL_E_INVALID_ARGUMENT; }
-  if (v4) k_mask_cols4<<<grid_for(lanes), kBlock, 0, s>>>(a, send, keep0, keep1, rows, cols, seed, ctr0);
+  if (v4) {
+    uint32_t dm;
+    int ds;
+    group_magic(lanes, cols / 4, &dm, &ds);
+    EFL_MASK_LAUNCH(g_mask_blocks[2].load(std::memory_order_relaxed), g_mask_store[2].load(std::memory_order_relaxed),
+                    lanes, s, EFL_K_COLS4, a, send, keep0, keep1, rows, cols, seed, ctr0, dm, ds);
+  }
   else k_mask_cols2<<<grid_for(lanes), kBlock, 0, s>>>(a, send, keep0, keep1, rows, cols, seed, ctr0);
   return hip_status(hipGetLastError(), "efl_ss_mask_cols");
 }
@@ -402,8 +615,13 @@ EFL_API int efl_ss_mask_rows(const float* b, float* send, float* keep0, float* k
   const bool v4 = cols % 4 == 0 && aligned(b, 16) && aligned(send, 16) && aligned(keep0, 16) && aligned(keep1, 16);
   const long long lanes = (rows / 2) * (v4 ? cols / 4 : cols);
   if (!lanes_ok(lanes)) { set_error("efl_ss_mask_rows: tensor too large"); return EFL_E_INVALID_ARGUMENT; }
-  if (v4) k_mask_rows<4><<<grid_for(lanes), kBlock, 0, s>>>(b, send, keep0, keep1, rows, cols, seed, ctr0);
-  else k_mask_rows<1><<<grid_for(lanes), kBlock, 0, s>>>(b, send, keep0, keep1, rows, cols, seed, ctr0);
+  uint32_t dm;
+  int ds;
+  group_magic(lanes, v4 ? cols / 4 : cols, &dm, &ds);
+  if (v4)
+    EFL_MASK_LAUNCH(g_mask_blocks[3].load(std::memory_order_relaxed), g_mask_store[3].load(std::memory_order_relaxed),
+                    lanes, s, EFL_K_ROWS4, b, send, keep0, keep1, rows, cols, seed, ctr0, dm, ds);
+  else k_mask_rows<1, 1, 0><<<grid_for(lanes), kBlock, 0, s>>>(b, send, keep0, keep1, rows, cols, seed, ctr0, dm, ds);
   return hip_status(hipGetLastError(), "efl_ss_mask_rows");
 }
 

@@ -11,6 +11,7 @@
 // the exponentiation base, the fixed-base table entry, running products. All G lanes read the
 // same word (broadcast); the E elements of the wave hit consecutive banks.
 #include <atomic>
+#include <type_traits>
 
 #include "pl_common.h"
 #include "sliced.h"
@@ -1397,12 +1398,104 @@ __device__ __forceinline__ void m_func(uint32_t (&res)[C / 2], const uint32_t* _
   // keep the key constants the code after the exponentiation needs from being loaded (and held
   // in VGPRs) across it: the loop wants its registers for the accumulators
   asm volatile("" ::: "memory");
+  // the running value's limb layout: folded (symmetric squarings, sliced28.h) for the 32-word-slice
+  // families over G >= 2 lanes (the 2048- to 8192-bit keys' defaults, 37-limb slices), blocked
+  // otherwise (the short-slice families keep CIOS: their unrolled folded loops cost compile time
+  // for little)
+  constexpr bool kFold = G > 1 && C == 32 && EFL_SQR_FOLD;
+  const uint32_t minv28 = second ? k.d.q2_minv28 : k.d.p2_minv28;
+  const uint32_t* r2_28 = k.at(second ? k.d.off_q2_r2_28[kLog2G] : k.d.off_p2_r2_28[kLog2G]);
+  const uint32_t* m28_at = k.at(second ? k.d.off_q2_28 : k.d.off_p2_28);
+  if constexpr (kFold) {
+    uint32_t a[C28], m28[C28];
+    s28::from_words_folded<C28, G>(a, SCR, E, L, g);
+    s28::slice_uniform_folded<C28, G>(m28, m28_at, g);
+    s28::mont_mul_folded<C28, G>(a, Uniform{r2_28}, BASE, E, m28, minv28, g);   // c R28
+    lds_sync();
+    if (tab) {
+      constexpr int CP = pad4<C28>();
+      uint32_t* slot = tab + g * CP;               // entry e at slot + e * G * CP (folded slices)
+      store28<C28>(slot, a);
+      uint32_t c2[C28];
+#pragma unroll
+      for (int j = 0; j < C28; ++j) c2[j] = a[j];
+      s28::fold_mont<C28, G>(c2, SCR, E, m28, minv28, g, true);
+      lds_sync();
+      s28::to_lds_folded<C28, G>(BASE, E, g, c2);
+      lds_sync();
+#pragma unroll 1
+      for (int e2 = 1; e2 < kDecEntries; ++e2) {
+        s28::fold_mont<C28, G>(a, BASE, E, m28, minv28, g, false);
+        store28<C28>(slot + (size_t)e2 * G * CP, a);
+      }
+      lds_sync();
+      int b = ebits - 1;
+      int j = b - kDecWin + 1 > 0 ? b - kDecWin + 1 : 0;
+      while (!ebit(ex, j)) ++j;
+      uint32_t v = 0;
+      for (int t = b; t >= j; --t) v = (v << 1) | ebit(ex, t);
+      load28<C28>(a, slot + (size_t)(v >> 1) * G * CP);
+      b = j - 1;
+      // The window walk with one fold_mont call site for its squarings and multiplies alike: the
+      // next operation is planned at the top of the loop (a lone squaring for a 0 bit, or a window's
+      // squarings, then its multiply). The entry is loaded just before its multiply, not held in
+      // VGPRs across the squarings (the squaring needs them; the other wave on the SIMD covers the
+      // load, once per window)
+      size_t ent_at = 0;
+      int sq_left = 0;
+      bool mul_next = false;
+#pragma unroll 1
+      for (;;) {
+        if (sq_left == 0 && !mul_next) {
+          if (b < 0) break;
+          if (!ebit(ex, b)) {
+            sq_left = 1;
+            --b;
+          } else {
+            j = b - kDecWin + 1 > 0 ? b - kDecWin + 1 : 0;
+            while (!ebit(ex, j)) ++j;
+            v = 0;
+            for (int t = b; t >= j; --t) v = (v << 1) | ebit(ex, t);
+            ent_at = (size_t)(v >> 1) * G * CP;
+            sq_left = b - j + 1;
+            mul_next = true;
+            b = j - 1;
+          }
+        }
+        const bool sq = sq_left > 0;
+        if (!sq) {
+          uint32_t ent[C28];
+          load28<C28>(ent, slot + ent_at);
+          s28::to_lds_folded<C28, G>(BASE, E, g, ent);
+          lds_sync();
+        }
+        s28::fold_mont<C28, G>(a, sq ? SCR : BASE, E, m28, minv28, g, sq);
+        lds_sync();
+        if (sq) --sq_left;
+        else mul_next = false;
+      }
+    } else {
+      s28::to_lds_folded<C28, G>(BASE, E, g, a);
+      lds_sync();
+#pragma unroll 1
+      for (int b = ebits - 2; b >= 0; --b) {
+        s28::fold_mont<C28, G>(a, SCR, E, m28, minv28, g, true);
+        lds_sync();
+        if (ebit(ex, b)) {
+          s28::fold_mont<C28, G>(a, BASE, E, m28, minv28, g, false);
+          lds_sync();
+        }
+      }
+    }
+    s28::mont_mul_folded<C28, G>(a, Unit{}, BASE, E, m28, minv28, g);   // y = c^(x-1) mod x^2
+    lds_sync();
+    s28::to_lds_folded<C28, G>(SCR, E, g, a);
+    lds_sync();
+  } else {
   uint32_t a[C28], m28[C28];
   s28::from_words<C28>(a, SCR, E, L, g);
-  slice_uniform<C28>(m28, k.at(second ? k.d.off_q2_28 : k.d.off_p2_28), g);
-  const uint32_t minv28 = second ? k.d.q2_minv28 : k.d.p2_minv28;
-  s28::mont_mul<C28, G>(a, Uniform{k.at(second ? k.d.off_q2_r2_28[kLog2G] : k.d.off_p2_r2_28[kLog2G])}, m28,
-                        minv28, g);
+  slice_uniform<C28>(m28, m28_at, g);
+  s28::mont_mul<C28, G>(a, Uniform{r2_28}, m28, minv28, g);
   lds_sync();
   if (tab) {
     constexpr int CP = pad4<C28>();
@@ -1465,6 +1558,7 @@ __device__ __forceinline__ void m_func(uint32_t (&res)[C / 2], const uint32_t* _
   lds_sync();
   to_lds<C28>(SCR, E, g, a);
   lds_sync();
+  }
   s28::to_words<C>(t, SCR, E, L28, g);
   lds_sync();
   asm volatile("" ::: "memory");
@@ -1950,6 +2044,92 @@ __global__ __launch_bounds__(kSlBlock, EFL_WALK1_WAVES) void k_crt_pair_tjoin(
   pair_join<C>(h, ox2, n2w, lds, out + el * 2 * C, q, valid);
 }
 
+// The tail as a product tree across lanes (round 6). The element-halves past the whole rounds are
+// split S ways over table rows INSIDE a wave: lane l walks rows [rows p / S, rows (p + 1) / S) of
+// element-half (l >> 5, (l & 31) / S), p = l % S, part 0 from the walk start (lane_gstart). The S
+// partial products then meet in log2 S levels: at level d the lanes with p % 2d == 0 take the
+// partner's (p + d) product through LDS and multiply, so an element-half's S - 1 products cost
+// log2 S products of wave time, where the split-and-join launches (k_crt_pair_part,
+// k_crt_pair_tjoin) paid P - 1 in series, in a second launch, plus each part's store and reload.
+// Part 0 then holds the element-half's walk, and the p / q halves join as in k_crt_pair_whole.
+// Lanes diverge only in the walk's trip count (rows differ by at most one) and in part 0's
+// lane_gstart; lds_sync is a wavefront fence, so the divergent calls are safe.
+template <int C, int S>
+__global__ __launch_bounds__(kSlBlock, EFL_WALK1_WAVES) void k_crt_pair_tree(
+    Key kp, Key kq, const uint32_t* __restrict__ n2w, const long long* __restrict__ m,
+    const uint32_t* __restrict__ a_in, uint32_t* __restrict__ out, long long N, long long el0, uint64_t seed,
+    long long ctr0) {
+  static_assert(S >= 2 && S <= 32 && (S & (S - 1)) == 0, "parts per element-half: a power of two dividing 32");
+  constexpr int E = kSlBlock, C28 = s28::limbs_per_lane(C, 1);
+  extern __shared__ uint32_t lds[];
+  const int lane = (int)threadIdx.x;
+  const bool q = lane >= 32;
+  const int part = lane % S;
+  const long long el = el0 + (long long)blockIdx.x * (32 / S) + (lane & 31) / S;
+  const bool live = el < N;
+  const Key k = q ? kq : kp;
+  uint32_t* B = lds + lane;
+  uint32_t* A = lds + C28 * E + lane;
+  uint32_t m28[C28], acc[C28];
+  slice_uniform<C28>(m28, k.at(k.d.off_n2_28), 0);
+  const uint32_t minv28 = k.d.n2_minv28;
+  bool have = false;
+  if (live) {
+    const int words = (k.d.a_bits + 31) >> 5;
+    if (part == 0) {
+      lane_gstart<C>(acc, k, m28, m ? m[el] : 0, B, E);
+      have = true;
+    }
+    if (a_in) {
+      for (int w = 0; w < words; ++w) A[w * E] = a_in[el * words + w];
+    } else {
+      draw_a<1>(A, E, words, k.d.a_bits, seed, (uint64_t)(ctr0 + el), 0);
+    }
+    lds_sync();
+    const int size = regroup_shared(A, E, words, k.d.group_size, 0);
+    const int rows = k.d.table_rows;
+    const int r0 = (int)((long long)rows * part / S), r1 = (int)((long long)rows * (part + 1) / S);
+    have = walk28_rows<C, 1>(acc, k, A, B, E, words, size, m28, 0, r0, r1, have);
+  }
+  for (int d = 1; d < S; d <<= 1) {
+    lds_sync();
+#pragma unroll
+    for (int j = 0; j < C28; ++j) B[j * E] = acc[j];
+    A[0] = have ? 1u : 0u;
+    lds_sync();
+    if (live && part % (2 * d) == 0 && A[d]) {
+      uint32_t b[C28];
+#pragma unroll
+      for (int j = 0; j < C28; ++j) b[j] = B[j * E + d];
+      if (have) {
+        s28::mul_fips1<C28>(acc, b, m28, minv28);
+      } else {
+#pragma unroll
+        for (int j = 0; j < C28; ++j) acc[j] = b[j];
+        have = true;
+      }
+    }
+  }
+  const bool valid = live && part == 0;
+  uint32_t h[C];
+  lds_sync();
+  if (valid) {
+    s28::mont_mul<C28, 1>(acc, Unit{}, m28, minv28, 0);
+    to_lds<C28>(B, E, 0, acc);
+  }
+  lds_sync();
+  if (valid) s28::to_words<C>(h, B, E, C28, 0);
+  lds_sync();
+  const uint32_t* ox2 = q ? kp.at(kp.d.off_n2) : kq.at(kq.d.off_n2);   // the other prime's square
+  pair_join<C>(h, ox2, n2w, lds, out + (valid ? el : 0) * 2 * C, q, valid);
+}
+
+// efl_pl_tune(ln, 6, v): the tail of the paired CRT encryption: 0 / 1 = the split-and-join launches
+// (round 5; tail_parts chooses the parts, 1 when the tail is not worth splitting), 2 / 4 / 8 / 16 = the
+// product tree across lanes with that S (round 6: bit-identical, measured no faster at the MNIST shape,
+// DESIGN.md §6a, so not the default)
+std::atomic<int> g_crt_tail{0};
+
 // efl_pl_tune(ln, 5, v): the key owner's CRT encryption, 0 = chosen per launch (the paired lanes
 // whenever they apply), 1 = one launch per sub-key and the join launch, 2 = the paired lanes
 std::atomic<int> g_crt_fused{0};
@@ -1977,6 +2157,7 @@ int tail_parts(long long waves, int rows, long long* whole, double* cost) {
   return bp;
 }
 
+
 template <int C>
 hipError_t run_crt_pair(const Key& kp, const Key& kq, const uint32_t* n2w, const long long* m, const uint32_t* a,
                         uint32_t* out, long long N, uint64_t seed, long long ctr0, hipStream_t s) {
@@ -1984,8 +2165,15 @@ hipError_t run_crt_pair(const Key& kp, const Key& kq, const uint32_t* n2w, const
   const long long waves = (N + 31) / 32;
   long long whole = 0;
   double cost = 0.0;
-  int parts = tail_parts(waves, kp.d.table_rows, &whole, &cost);
-  if (parts == 1) whole = waves;
+  const int S = g_crt_tail.load(std::memory_order_relaxed);   // >= 2: the tree tail with S parts
+  const bool tree = S >= 2;
+  int parts = 1;
+  if (tree) {
+    whole = waves / simd_count() * simd_count();   // the whole rounds; the rest is the tree tail
+  } else {
+    parts = tail_parts(waves, kp.d.table_rows, &whole, &cost);
+    if (parts == 1) whole = waves;
+  }
   const long long tw = waves - whole;
   const int aw = (kp.d.a_bits + 31) / 32;
   // LDS: the walk's columns (C28 + aw words per lane), at least the join's (2 C + 1) x 32 words
@@ -1998,6 +2186,21 @@ hipError_t run_crt_pair(const Key& kp, const Key& kq, const uint32_t* n2w, const
     err = hipGetLastError();
   }
   if (err != hipSuccess || tw == 0) return err;
+  if (tree) {
+    const long long el0 = whole * 32, tail_el = N - el0;
+    const unsigned grid = (unsigned)((tail_el * S + 31) / 32);
+    switch (S) {
+      case 2: hipLaunchKernelGGL((k_crt_pair_tree<C, 2>), dim3(grid), dim3(kSlBlock), lds, s, kp, kq, n2w, m, a, out, N,
+                                 el0, seed, ctr0); break;
+      case 4: hipLaunchKernelGGL((k_crt_pair_tree<C, 4>), dim3(grid), dim3(kSlBlock), lds, s, kp, kq, n2w, m, a, out, N,
+                                 el0, seed, ctr0); break;
+      case 8: hipLaunchKernelGGL((k_crt_pair_tree<C, 8>), dim3(grid), dim3(kSlBlock), lds, s, kp, kq, n2w, m, a, out, N,
+                                 el0, seed, ctr0); break;
+      default: hipLaunchKernelGGL((k_crt_pair_tree<C, 16>), dim3(grid), dim3(kSlBlock), lds, s, kp, kq, n2w, m, a, out,
+                                  N, el0, seed, ctr0); break;
+    }
+    return hipGetLastError();
+  }
   const size_t slots = (size_t)tw * parts * kSlBlock;
   uint32_t* P = nullptr;
   err = hipMallocAsync(reinterpret_cast<void**>(&P), slots * CP * 4 + slots, s);
@@ -2219,6 +2422,9 @@ hipError_t sl_crt_encrypt_pair(const Key& kp, const Key& kq, int C, const uint32
 }
 int sl_crt_fused(int v) {
   return v < 0 ? g_crt_fused.load() : g_crt_fused.exchange(v);
+}
+int sl_crt_tail(int v) {
+  return v < 0 ? g_crt_tail.load() : g_crt_tail.exchange(v);
 }
 hipError_t sl_add(const Key& k, int C, const uint32_t* x, const uint32_t* y, uint32_t* out, long long N,
                   hipStream_t s) {

@@ -181,6 +181,7 @@ hipError_t sl_fbpowm(const Key& k, int C, const uint32_t* a, uint32_t* out, long
 hipError_t sl_fbpowm_g(const Key& k, int C, const long long* m, const uint32_t* a, uint32_t* out, long long N,
                        uint64_t seed, long long ctr0, hipStream_t s);
 int sl_crt_fused(int v);
+int sl_crt_tail(int v);
 // the key owner's whole CRT encryption (or hs^(a') for m NULL) with an element's two walks in one
 // wave and the CRT join at its end: the ciphertext mod n^2 (n2w = n^2 in 32-bit words) into out
 // ([N][2 C] words). hipErrorNotSupported unless the one-lane family C = 32 serves both sub-keys

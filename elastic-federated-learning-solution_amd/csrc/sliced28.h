@@ -33,6 +33,11 @@ namespace s28 {
 #define EFL_MONT28_UNROLL 2
 #endif
 
+// Decryption squarings of numbers over G >= 2 lanes in the folded layout, symmetric (round 6; build
+// knob for A/B: EFL_SQR_FOLD=0 builds the blocked CIOS squaring)
+#ifndef EFL_SQR_FOLD
+#define EFL_SQR_FOLD 0
+#endif
 // One-lane squarings by product scanning (sqr_fips1) instead of CIOS through LDS (build knob for
 // A/B: EFL_SQR_FIPS=0 builds the round-2 squaring)
 #ifndef EFL_SQR_FIPS
@@ -255,6 +260,239 @@ __device__ __forceinline__ void mont_sqr(uint32_t (&a)[C], uint32_t* scratch, in
   }
 }
 
+// ---- folded layout and symmetric squaring (round 6; the G >= 2 decryption families) -----------
+// Squaring by CIOS forms every cross product a_i a_j twice (steps i and j). Forming 2 a_i a_j once,
+// at step min(i, j), and a_i^2 at step i gives every column c all its terms by step c, so the
+// reduction digits u and the result are those of CIOS exactly (tools: the round-6 simulation in
+// DESIGN.md §5). But in SIMD a step's products only shrink if the limbs at or above i are spread
+// over the lanes: with the blocked layout (lane g: limbs g C .. g C + C - 1) the top lane stays busy
+// until the last chunk and the square saves 1/(2G) of its products. FOLDED: lane g holds a low chunk
+// (positions H1 g + j, j < H1 = ceil(C / 2)) and a high chunk (positions G H1 + H2 (G - 1 - g) + j,
+// j < H2 = floor(C / 2)). While i is in the low half every lane's high chunk lies above i (all
+// doubled products), the low slots of lanes past i's chunk are doubled, i's own slot single, the
+// slots below zero; in the high half no low slot has products at all. A squaring then issues
+// (L/2)(C + C) + (L/2)(H2 + C) limb products instead of 2 L C: 7/8 of CIOS's, the product half
+// 3/4. The accumulator shift crosses chunks in position order: a low chunk's top takes the next
+// lane's low bottom (lane G-1: its own high bottom), a high chunk's top the previous lane's high
+// bottom (lane 0: zero), so a step moves two 64-bit values between lanes (from_next64,
+// from_prev64). Bounds as mont_mul: a step adds < 2^57 (doubled product) + 2^56 (m u) to a
+// position, < 2^64 over the 64 steps between lazy normalisations.
+constexpr __host__ __device__ int fold_h1(int C) { return (C + 1) / 2; }
+constexpr __host__ __device__ int fold_h2(int C) { return C / 2; }
+// position of folded slot j (j < H1: low chunk; else high chunk) of lane g
+template <int C, int G>
+__device__ __forceinline__ int fold_pos(int g, int j) {
+  constexpr int H1 = fold_h1(C), H2 = fold_h2(C);
+  return j < H1 ? H1 * g + j : G * H1 + H2 * (G - 1 - g) + (j - H1);
+}
+
+template <int C, int G>
+__device__ __forceinline__ void to_lds_folded(uint32_t* base, int E, int g, const uint32_t (&x)[C]) {
+#pragma unroll
+  for (int j = 0; j < C; ++j) base[fold_pos<C, G>(g, j) * E] = x[j];
+}
+template <int C, int G>
+__device__ __forceinline__ void from_lds_folded(uint32_t (&x)[C], const uint32_t* base, int E, int g) {
+#pragma unroll
+  for (int j = 0; j < C; ++j) x[j] = base[fold_pos<C, G>(g, j) * E];
+}
+template <int C, int G>
+__device__ __forceinline__ void slice_uniform_folded(uint32_t (&x)[C], const uint32_t* __restrict__ p, int g) {
+#pragma unroll
+  for (int j = 0; j < C; ++j) x[j] = p[fold_pos<C, G>(g, j)];
+}
+
+// accumulators (folded) -> normalised 28-bit limbs: the carry ripples through the 2G chunks in
+// position order (low chunks of lanes 0 .. G-1, then the high chunks of lanes G-1 .. 0)
+template <int C, int G>
+__device__ __forceinline__ void normalize_folded(uint32_t (&a)[C], const uint64_t (&T)[C], int g) {
+  constexpr int H1 = fold_h1(C);
+  uint64_t cl = 0, ch = 0;
+#pragma unroll
+  for (int j = 0; j < H1; ++j) {
+    const uint64_t v = T[j] + cl;
+    a[j] = (uint32_t)v & kMask;
+    cl = v >> kBits;
+  }
+#pragma unroll
+  for (int j = H1; j < C; ++j) {
+    const uint64_t v = T[j] + ch;
+    a[j] = (uint32_t)v & kMask;
+    ch = v >> kBits;
+  }
+  // 2G - 1 rounds carry a chunk's carry into the next chunk in position order
+#pragma unroll
+  for (int r = 0; r < 2 * G - 1; ++r) {
+    uint64_t inl = from_prev64<G>(cl);
+    if (g == 0) inl = 0;
+    uint64_t inh = from_next64<G>(ch);
+    if (g == G - 1) inh = cl;          // lane G-1's high chunk follows its own low chunk
+#pragma unroll
+    for (int j = 0; j < H1; ++j) {
+      const uint64_t v = (uint64_t)a[j] + inl;
+      a[j] = (uint32_t)v & kMask;
+      inl = v >> kBits;
+    }
+#pragma unroll
+    for (int j = H1; j < C; ++j) {
+      const uint64_t v = (uint64_t)a[j] + inh;
+      a[j] = (uint32_t)v & kMask;
+      inh = v >> kBits;
+    }
+    cl = inl;
+    ch = g == 0 ? 0 : inh;             // the top chunk's carry out is 0: the number is < R
+  }
+}
+
+template <int C, int G>
+__device__ __forceinline__ void lazy_normalize_folded(uint64_t (&T)[C], int g) {
+  constexpr int H1 = fold_h1(C);
+  uint64_t cl = 0, ch = 0;
+#pragma unroll
+  for (int j = 0; j < H1; ++j) {
+    const uint64_t v = T[j] + cl;
+    T[j] = v & kMask;
+    cl = v >> kBits;
+  }
+#pragma unroll
+  for (int j = H1; j < C; ++j) {
+    const uint64_t v = T[j] + ch;
+    T[j] = v & kMask;
+    ch = v >> kBits;
+  }
+  uint64_t inl = from_prev64<G>(cl);
+  if (g == 0) inl = 0;
+  uint64_t inh = from_next64<G>(ch);
+  if (g == G - 1) inh = cl;
+  T[0] += inl;
+  T[H1] += inh;                        // values stay lazy (< 2^37) but far from overflow
+}
+
+// one CIOS step in the folded layout: bi the step's b limb, mul the multipliers of the low and high
+// slots (LOW = false: the low slots take no product), then the reduction and the shift. No lazy
+// normalisation here: the callers normalise between chunks (a branch inside the unrolled steps
+// split them into blocks, and the compiler then moved every accumulator each step)
+template <int C, int G, bool LOW>
+__device__ __forceinline__ void fold_step(uint64_t (&T)[C], const uint32_t (&mul)[C], uint32_t bi,
+                                          const uint32_t (&m)[C], uint32_t minv, int g) {
+  constexpr int H1 = fold_h1(C);
+  if constexpr (LOW) {
+#pragma unroll
+    for (int j = 0; j < H1; ++j) T[j] = (uint64_t)mul[j] * bi + T[j];
+  }
+#pragma unroll
+  for (int j = H1; j < C; ++j) T[j] = (uint64_t)mul[j] * bi + T[j];
+  const uint32_t u = sl::bcast0<G>(((uint32_t)T[0] * minv) & kMask);
+#pragma unroll
+  for (int j = 0; j < C; ++j) T[j] = (uint64_t)m[j] * u + T[j];
+  uint64_t nl = from_next64<G>(T[0]);
+  nl = g == G - 1 ? T[H1] : nl;
+  uint64_t nh = from_prev64<G>(T[H1]);
+  nh = g == 0 ? 0ull : nh;
+  const uint64_t c0 = g == 0 ? T[0] >> kBits : 0ull;   // lane 0: the bottom limb is now 0 mod 2^28
+#pragma unroll
+  for (int j = 0; j < H1 - 1; ++j) T[j] = T[j + 1];
+  T[H1 - 1] = nl;
+#pragma unroll
+  for (int j = H1; j < C - 1; ++j) T[j] = T[j + 1];
+  T[C - 1] = nh;
+  T[0] += c0;
+}
+
+// The L steps of a folded product (SQ = false: mul = a, every product) or square (SQ: mul = 2 a,
+// the diagonal halved when its step comes and the slot zeroed after it; the high half's steps skip
+// the low slots, all zero by then). Steps run a chunk at a time, unrolled (the low accumulators'
+// shift is a full rotation per chunk: no moves), and the accumulators are lazily normalised between
+// chunks, before any position could have gone 64 steps without one.
+template <int C, int G, bool SQ>
+__device__ __forceinline__ void fold_pass(uint64_t (&T)[C], uint32_t (&mul)[C], const uint32_t* bl, int E,
+                                          const uint32_t (&m)[C], uint32_t minv, int g) {
+  constexpr int H1 = fold_h1(C), H2 = fold_h2(C), L = C * G;
+  static_assert(H1 <= 64, "chunk longer than the lazy-normalisation bound");
+  int since = 0;
+#pragma unroll 1
+  for (int c = 0; c < G; ++c) {        // i in the low chunk of lane c
+#pragma unroll
+    for (int s = 0; s < H1; ++s) {
+      const uint32_t bi = bl[(c * H1 + s) * E];
+      const bool diag = SQ && g == c;
+      if constexpr (SQ) mul[s] = diag ? mul[s] >> 1 : mul[s];   // the diagonal a_i^2, once
+      fold_step<C, G, true>(T, mul, bi, m, minv, g);
+      if constexpr (SQ) mul[s] = diag ? 0u : mul[s];            // below every later step
+    }
+    since += H1;
+    if (L > 64 && since + H1 > 64) {
+      lazy_normalize_folded<C, G>(T, g);
+      since = 0;
+    }
+  }
+#pragma unroll 1
+  for (int c = 0; c < G; ++c) {        // i in the high chunk of lane G - 1 - c
+#pragma unroll
+    for (int s = 0; s < H2; ++s) {
+      const uint32_t bi = bl[(G * H1 + c * H2 + s) * E];
+      const bool diag = SQ && g == G - 1 - c;
+      if constexpr (SQ) mul[H1 + s] = diag ? mul[H1 + s] >> 1 : mul[H1 + s];
+      fold_step<C, G, !SQ>(T, mul, bi, m, minv, g);   // a square's low slots are all zero here
+      if constexpr (SQ) mul[H1 + s] = diag ? 0u : mul[H1 + s];
+    }
+    since += H2;
+    if (L > 64 && since + H2 > 64) {
+      lazy_normalize_folded<C, G>(T, g);
+      since = 0;
+    }
+  }
+}
+
+// a <- a b R^-1 mod m with b limb i read from the element's LDS array bl (position order), or, sq
+// set, a <- a^2 R^-1 mod m (a is first written to bl). The exponentiation calls it at one site for
+// its squarings and multiplies alike.
+template <int C, int G>
+__device__ __forceinline__ void fold_mont(uint32_t (&a)[C], uint32_t* bl, int E, const uint32_t (&m)[C],
+                                          uint32_t minv, int g, bool sq) {
+  uint64_t T[C];
+#pragma unroll
+  for (int j = 0; j < C; ++j) T[j] = 0;
+  uint32_t mul[C];
+  if (sq) {
+    to_lds_folded<C, G>(bl, E, g, a);
+    sl::lds_sync();
+#pragma unroll
+    for (int j = 0; j < C; ++j) mul[j] = a[j] << 1;   // < 2^29
+    fold_pass<C, G, true>(T, mul, bl, E, m, minv, g);
+  } else {
+#pragma unroll
+    for (int j = 0; j < C; ++j) mul[j] = a[j];
+    fold_pass<C, G, false>(T, mul, bl, E, m, minv, g);
+  }
+  normalize_folded<C, G>(a, T, g);
+}
+
+// the constant b of a folded product (a uniform number, or 1 for the conversion out) goes to the
+// element's LDS array first, so every product runs through fold_mont
+template <int C, int G, class B>
+__device__ __forceinline__ void mont_mul_folded(uint32_t (&a)[C], const B& b, uint32_t* bl, int E,
+                                                const uint32_t (&m)[C], uint32_t minv, int g) {
+  sl::lds_sync();
+  for (int i = g; i < C * G; i += G) bl[i * E] = b(i);
+  sl::lds_sync();
+  fold_mont<C, G>(a, bl, E, m, minv, g, false);
+}
+
+// the element's number in 32-bit words in LDS (word k at w32[k * E], L32 words) -> this lane's
+// folded 28-bit limbs
+template <int C, int G>
+__device__ __forceinline__ void from_words_folded(uint32_t (&a)[C], const uint32_t* w32, int E, int L32, int g) {
+#pragma unroll
+  for (int j = 0; j < C; ++j) {
+    const int bit = kBits * fold_pos<C, G>(g, j);
+    const int w = bit >> 5, sft = bit & 31;
+    const uint32_t lo = w < L32 ? w32[w * E] : 0u;
+    const uint32_t hi = w + 1 < L32 ? w32[(w + 1) * E] : 0u;
+    a[j] = (uint32_t)((((uint64_t)hi << 32) | lo) >> sft) & kMask;
+  }
+}
+
 // The element's number in 32-bit words in LDS (word k at w32[k * E], L32 words) -> this lane's
 // 28-bit limbs. Words past L32 read as 0.
 template <int C>
@@ -282,6 +520,7 @@ __device__ __forceinline__ void to_words(uint32_t (&w)[C32], const uint32_t* l28
     w[j] = (uint32_t)((l0 | (l1 << kBits) | (l2 << (2 * kBits))) >> s);
   }
 }
+
 
 }  // namespace s28
 }  // namespace efl

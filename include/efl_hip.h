@@ -80,8 +80,11 @@ const char* efl_last_error(void);
  * Philox blocks per lane of efl_dp_noise (1, 2, 4; default 4); kinds 21-24 = the fp64 encode's
  * workgroup size (128, 256, 512, 1024), units per lane (1, 2), nontemporal mask (as kind 4) and
  * XCD-aware tile order (0 / 1).
- * Batched tile defaults (kinds 10-13): encode 512 lanes x 1 pair, decode 512 x 2; value -1 on
- * kinds 10-13 reads the current value without changing it.
+ * kind 25 = lane groups (Philox blocks) per lane of efl_ss_noise / efl_ss_mask_cols /
+ * efl_ss_mask_rows (1, 2, 4), kind 28 their store flavour (0 plain, 2 nontemporal, 7 `nt sc1`): each
+ * has a per-kernel default; setting a value sets all kernels, -2 restores the defaults; kinds 26 / 27
+ * = tiles per workgroup of the batched encode / decode (1, 2, 4, 8). Batched tile defaults (kinds 10-13): encode 512 lanes x 1 pair,
+ * decode 512 x 2. Value -1 on kinds 10-13, 20 and 25 reads the current value without changing it.
  * Returns the previous value or EFL_E_INVALID_ARGUMENT. */
 int efl_fxp_tune(int kind, int value);
 

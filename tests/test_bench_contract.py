@@ -1,5 +1,5 @@
 """The BENCH line's contract (the driver parses bench.py's one JSON line), checked on the line the
-final round-5 build printed on the MI355X box (profiles/r05/bench.json) and on the code that makes
+final round-6 build printed on the MI355X box (profiles/r06/bench.json) and on the code that makes
 it: every required key, the roofline and cpu_baseline objects, and their internal consistency."""
 import json
 import os
@@ -11,7 +11,7 @@ REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step
 
 
 def _line():
-    with open(os.path.join(ROOT, "profiles", "r05", "bench.json")) as f:
+    with open(os.path.join(ROOT, "profiles", "r06", "bench.json")) as f:
         lines = [ln for ln in f.read().splitlines() if ln.startswith("{")]
     assert len(lines) == 1
     return json.loads(lines[0])
@@ -55,11 +55,26 @@ def test_rank_devices_reported():
     assert d["devices_used"] == len({(r["host"], r["pci"]) for r in rd})
 
 
+def test_rank_devices_carry_each_ranks_kernels():
+    """Each rank's own kernel times and roofline fractions, beside its device:
+    frac = kernel bytes / time / peak, so a slow rank is visible in the line, not only the max."""
+    d = _line()
+    for r in d["rank_devices"]:
+        km, fr = r["kernels_ms"], r["roofline_frac"]
+        assert km["encode"] > 0 and km["decode"] > 0 and r["step_ms"] > 0
+        for k in ("encode", "decode"):
+            want = 20 * 65536 * 1024 / (km[k] * 1e-3) / 1e9 / 8000.0
+            assert abs(fr[k] - want) < 2e-3 * want + 1e-3, (k, fr[k], want)
+
+
 def test_config3_both_layouts_reported():
     c3 = _line()["config3"]
     assert c3["roundtrip_ok"] and c3["views"]["roundtrip_ok"]
     assert c3["table_entries"] == {"encode": 4096, "decode": 4096}
     assert c3["views"]["table_entries"] == {"encode": 1, "decode": 1}
+    # per-launch batched kernel times (VERDICT r5 item 1) and the tile each direction ran with
+    assert c3["kernels_ms"]["encode"] > 0 and c3["kernels_ms"]["decode"] > 0
+    assert set(c3["tile_lanes_pairs"]) == {"encode", "decode"}
 
 
 def test_pmc_traffic_names_the_shipping_library():
@@ -86,7 +101,7 @@ def test_records_come_from_the_shipping_library():
     and the Stage P report carries the GMP CPU baseline of the same run (bench hygiene)."""
     h = _src_hash()
     assert _line()["library"].endswith("src " + h)
-    with open(os.path.join(ROOT, "profiles", "r05", "bench_stage_p.jsonl")) as f:
+    with open(os.path.join(ROOT, "profiles", "r06", "bench_stage_p.jsonl")) as f:
         lines = [json.loads(ln) for ln in f if ln.startswith("{")]
     assert len(lines) == 3
     for d in lines:

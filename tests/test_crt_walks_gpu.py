@@ -116,3 +116,31 @@ def test_extreme_plaintexts(efl, owner):
             out[v] = owner.encrypt(m, counter_base=77)
     assert torch.equal(out[1].tensor.limbs, out[2].tensor.limbs)
     assert torch.equal(owner.decrypt(out[2], dtype=torch.int64), m)
+
+
+@pytest.mark.parametrize("tail", [0, 1, 2, 4, 8, 16])
+@pytest.mark.parametrize("n", [1, 17, 65, 2048, 100352, 100352 + 5 * 64 + 3])
+def test_tree_tail_equals_per_key(efl, owner, tail, n):
+    """The tail past the whole rounds as a product tree across lanes (efl_pl_tune(ln, 6, v): 2-16 a
+    fixed S) or as the round-5 split-and-join launches (0, the default, and 1): ciphertexts and
+    hs^(a') equal the per-key walks' bit for bit, for tails of every size (a lone element, a part-empty
+    wave, the MNIST activation's 2,048 elements, and a count whose tail is neither)."""
+    lib = efl.lib.raw()
+    g = torch.Generator(device="cuda").manual_seed(n + 1)
+    m = torch.randint(-2**40, 2**40, (n,), dtype=torch.int64, device="cuda", generator=g)
+    with mode(efl, 1):
+        want = (owner.encrypt(m, counter_base=7).tensor.limbs, owner.fbpowm(n=n, counter_base=9).limbs)
+    prev = lib.efl_pl_tune(16, 6, tail)
+    assert prev >= 0
+    try:
+        with mode(efl, 2):
+            got = (owner.encrypt(m, counter_base=7).tensor.limbs, owner.fbpowm(n=n, counter_base=9).limbs)
+    finally:
+        lib.efl_pl_tune(16, 6, prev)
+    assert torch.equal(got[0], want[0]) and torch.equal(got[1], want[1])
+
+
+def test_tree_tail_knob(efl):
+    lib = efl.lib.raw()
+    assert lib.efl_pl_tune(16, 6, -1) == 0               # split and join by default; the tree on request
+    assert lib.efl_pl_tune(16, 6, 3) < 0 and lib.efl_pl_tune(16, 6, 32) < 0

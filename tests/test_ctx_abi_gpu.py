@@ -252,11 +252,20 @@ def test_failed_table_build_leaves_a_live_key(lib, monkeypatch):
         assert _info(lib, c)["has_table"] == 0
         mag = torch.empty((N, ln), dtype=torch.int32, device="cuda")
         neg = torch.empty(N, dtype=torch.int8, device="cuda")
-        # the CRT route and decryption still run on the live block
-        ok(lib, lib.efl_pl_ctx_encrypt(c.h, m.data_ptr(), None, ct.data_ptr(), N, 5, 0, 0, stream()))
+        # the CRT sub-tables' build fails too (the injection covers every table build): the owner's
+        # route reports it, and the key block stays live for decryption
+        rc = lib.efl_pl_ctx_encrypt(c.h, m.data_ptr(), None, ct.data_ptr(), N, 5, 0, 0, stream())
+        assert rc == -8
+        hsa = torch.zeros((N, 2 * ln), dtype=torch.int32, device="cuda")
+        hsa[:, 0] = 1                                              # hsa = 1: the ciphertext is g(m)
+        ok(lib, lib.efl_pl_ctx_encrypt(c.h, m.data_ptr(), hsa.data_ptr(), ct.data_ptr(), N, 5, 0, 0, stream()))
         ok(lib, lib.efl_pl_ctx_decrypt(c.h, ct.data_ptr(), mag.data_ptr(), neg.data_ptr(), N, stream()))
         assert [(-x if s else x) for x, s in zip(ints(mag), neg.cpu().tolist())] == m.cpu().tolist()
         monkeypatch.delenv("EFL_PL_FAIL_TABLE_BUILD")
+        # the CRT route once the builds succeed, and its ciphertexts decrypt
+        ok(lib, lib.efl_pl_ctx_encrypt(c.h, m.data_ptr(), None, ct.data_ptr(), N, 5, 0, 0, stream()))
+        ok(lib, lib.efl_pl_ctx_decrypt(c.h, ct.data_ptr(), mag.data_ptr(), neg.data_ptr(), N, stream()))
+        assert [(-x if s else x) for x, s in zip(ints(mag), neg.cpu().tolist())] == m.cpu().tolist()
         ct2 = torch.empty_like(ct)
         ok(lib, lib.efl_pl_ctx_encrypt(c.h, m.data_ptr(), None, ct2.data_ptr(), N, 5, 0, 1, stream()))
         assert torch.equal(ct2, ct) and _info(lib, c)["has_table"] == 1
@@ -272,33 +281,42 @@ def test_failed_table_build_leaves_a_live_key(lib, monkeypatch):
 
 def test_public_then_private_gives_crt_the_whole_budget(lib):
     """the reference's usual order (SetPaillierPublicKey, then SetPaillierPrivateKey). The
-    public step builds the n^2 table; the owner's first encryption builds the CRT sub-keys and
-    releases that table, so the sub-tables get the windows efl_pl_set_keypair gives them (not the
-    few MB the n^2 table left), and the ciphertexts are the public path's."""
+    public step builds the n^2 table; when keeping it would narrow the CRT sub-tables' window (a
+    binding process budget), the owner's first encryption releases it and the sub-tables get the
+    windows efl_pl_set_keypair gives them; with room for both (a budget that does not bind) the
+    table stays. Either way the ciphertexts are the public path's."""
     k = KEYS[0]
     ln = k["n_bytes"] // 4
-    a, b = Ctx(lib), Ctx(lib)
+    used0 = i64(0)
+    prev = lib.efl_pl_table_budget(-1, ctypes.byref(used0))
+    N = 128
+    m = torch.randint(-2**40, 2**40, (N,), dtype=torch.int64, device="cuda")
+    lib.efl_pl_set_keypair.argtypes = [vp, cp, i32, cp, i32, i32, cp, cp, vp]
     try:
-        lib.efl_pl_set_keypair.argtypes = [vp, cp, i32, cp, i32, i32, cp, cp, vp]
-        ok(lib, lib.efl_pl_set_keypair(a.h, k["n"].encode(), k["n_bytes"], k["hs"].encode(), k["a_bits"] // 8, 1,
-                                       k["p"].encode(), k["q"].encode(), stream()))
-        assert lib.efl_pl_ctx_prepare(a.h, 2, stream()) == 1
-        want = _info(lib, a)["crt_table_window"]
-        a.close()
-        ok(lib, lib.efl_pl_set_public(b.h, k["n"].encode(), k["n_bytes"], k["hs"].encode(), k["a_bits"] // 8, 1,
-                                      stream()))
-        assert _info(lib, b)["has_table"] == 1
-        ok(lib, lib.efl_pl_set_private(b.h, k["p"].encode(), k["q"].encode(), stream()))
-        N = 128
-        m = torch.randint(-2**40, 2**40, (N,), dtype=torch.int64, device="cuda")
-        c1 = torch.empty((N, 2 * ln), dtype=torch.int32, device="cuda")
-        c2 = torch.empty_like(c1)
-        ok(lib, lib.efl_pl_ctx_encrypt(b.h, m.data_ptr(), None, c1.data_ptr(), N, 9, 3, 0, stream()))
-        inf = _info(lib, b)
-        assert inf["crt"] == 1 and inf["has_table"] == 0 and inf["table_bytes"] == 0
-        assert inf["crt_table_window"] == want, (inf, want)
-        ok(lib, lib.efl_pl_ctx_encrypt(b.h, m.data_ptr(), None, c2.data_ptr(), N, 9, 3, 1, stream()))
-        assert torch.equal(c1, c2)
+        for budget, released in ((2 << 30, True), (64 << 30, False)):
+            lib.efl_pl_table_budget(used0.value + budget, None)
+            a, b = Ctx(lib), Ctx(lib)
+            try:
+                ok(lib, lib.efl_pl_set_keypair(a.h, k["n"].encode(), k["n_bytes"], k["hs"].encode(), k["a_bits"] // 8,
+                                               1, k["p"].encode(), k["q"].encode(), stream()))
+                assert lib.efl_pl_ctx_prepare(a.h, 2, stream()) == 1
+                want = _info(lib, a)["crt_table_window"]
+                a.close()
+                ok(lib, lib.efl_pl_set_public(b.h, k["n"].encode(), k["n_bytes"], k["hs"].encode(), k["a_bits"] // 8,
+                                              1, stream()))
+                assert _info(lib, b)["has_table"] == 1
+                ok(lib, lib.efl_pl_set_private(b.h, k["p"].encode(), k["q"].encode(), stream()))
+                c1 = torch.empty((N, 2 * ln), dtype=torch.int32, device="cuda")
+                c2 = torch.empty_like(c1)
+                ok(lib, lib.efl_pl_ctx_encrypt(b.h, m.data_ptr(), None, c1.data_ptr(), N, 9, 3, 0, stream()))
+                inf = _info(lib, b)
+                assert inf["crt"] == 1 and inf["has_table"] == (0 if released else 1), (budget, inf)
+                if released:
+                    assert inf["table_bytes"] == 0 and inf["crt_table_window"] == want, (inf, want)
+                ok(lib, lib.efl_pl_ctx_encrypt(b.h, m.data_ptr(), None, c2.data_ptr(), N, 9, 3, 1, stream()))
+                assert torch.equal(c1, c2)
+            finally:
+                a.close()
+                b.close()
     finally:
-        a.close()
-        b.close()
+        lib.efl_pl_table_budget(prev, None)

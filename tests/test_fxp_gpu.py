@@ -336,10 +336,12 @@ def test_batched_ragged(efl):
 
 
 @pytest.mark.parametrize("knob", [(10, 256), (10, 128), (11, 1), (11, 4), (12, 256), (12, 128), (13, 1), (13, 4),
-                                  (17, 1), (17, 2), (17, 3), (18, 1), (18, 2), (18, 3), (19, 7)])
+                                  (17, 1), (17, 2), (17, 3), (18, 1), (18, 2), (18, 3), (19, 7), (26, 2), (26, 4),
+                                  (26, 8), (27, 2), (27, 4), (27, 8)])
 def test_batched_tuning_variants_identical(efl, knob):
     """Every batched fp32 tile shape and tile order (efl_fxp_tune 10-13, 17-19: 2-D grid, flat,
-    flat XCD-aware, persistent walk and its workgroup count) gives the same bits; ragged sizes,
+    flat XCD-aware, persistent walk and its workgroup count; 26-27 tiles per workgroup) gives the
+    same bits; ragged sizes,
     tensors smaller than a tile, and (for the persistent walk with 7 workgroups) many tiles each."""
     lib = efl.lib.raw()
     if knob[0] == 19:
@@ -455,7 +457,8 @@ def test_batched_tables_coalescing_identical(efl, coalesce):
 # ------------------------------------------------------------------- full size (256 MiB)
 
 def test_full_size_properties(efl):
-    """BASELINE config 2 size (67,108,864 fp32): size-independent properties + sampled bits."""
+    """BASELINE config 2 size (67,108,864 fp32): size-independent properties, and every element of M,
+    E and the decoded y compared with the oracle's."""
     n = 1 << 26
     g = torch.Generator(device="cuda").manual_seed(0)
     x = torch.randn(n, device="cuda", generator=g)
@@ -476,9 +479,11 @@ def test_full_size_properties(efl):
     xs = host(x[idx])
     Mo, Eo = fxp.encode(xs)
     assert np.array_equal(host(M[idx]), Mo) and np.array_equal(host(E[idx]), Eo)
-    # checksum of the whole output against an oracle pass over the whole tensor
+    # every element against an oracle pass over the whole tensor (not a checksum), and
+    # the decode of the oracle's own mantissas / exponents against the GPU decode, bit for bit
     Mo_all, Eo_all = fxp.encode(host(x))
-    assert int(M.sum()) == int(Mo_all.sum()) and int(E.sum()) == int(Eo_all.sum())
+    assert np.array_equal(host(M), Mo_all) and np.array_equal(host(E), Eo_all)
+    assert np.array_equal(bits32(y), fxp.decode(Mo_all, Eo_all).view(np.uint32))
 
 
 # ------------------------------------------------- slices of the exhaustive fp32 sweep

@@ -125,3 +125,38 @@ def test_share_full_size_properties(ss):
     u = np.stack([mask.uniform(2024, int(b), 4) for b in (idx[::4] // 4).cpu().numpy()[:2000]])
     want = (u.reshape(-1) * xs[: u.size]).astype(np.float32)
     assert np.array_equal(bits(a[idx][: u.size]), nbits(want))
+
+
+@pytest.mark.parametrize("nb", [1, 2, 4])
+@pytest.mark.parametrize("st", [0, 2, 7])
+def test_mask_variants_identical(ss, nb, st):
+    """Every lane-group count (efl_fxp_tune 25) and store flavour (28) of the mask kernels gives the
+    oracle's bits, at sizes whose last lane groups are partial (the per-group tail path) and at sizes
+    that fill every group."""
+    import efl
+    lib = efl.lib.raw()
+    old = lib.efl_fxp_tune(25, nb), lib.efl_fxp_tune(28, st)
+    assert min(old) >= 0
+    try:
+        for n in (5, 4096 * 4 + 12, 4 * 256 * 4 * 3 + 4):
+            x = rand(n, n + nb)
+            for op, div in ((0, 1.0), (1, 1.0), (2, 3.0)):
+                got = ss._noise(torch.from_numpy(x).cuda(), op, div, stream=ss.NoiseStream(n, 9))
+                want = mask.noise(x, n, 9, op, div)
+                got = got if isinstance(got, tuple) else (got,)
+                want = want if isinstance(want, tuple) else (want,)
+                for g, w in zip(got, want):
+                    assert np.array_equal(bits(g), nbits(w)), (n, op)
+        for R, C in ((3, 8), (257, 1024), (100, 392)):
+            a = rand((R, C), R + C)
+            for g, w in zip(ss.mask_cols(torch.from_numpy(a).cuda(), stream=ss.NoiseStream(R, 1)),
+                            mask.mask_cols(a, R, 1)):
+                assert np.array_equal(bits(g), nbits(w)), (R, C)
+        for K, N in ((2, 4), (514, 1024), (392, 256)):
+            b = rand((K, N), K + N)
+            for g, w in zip(ss.mask_rows(torch.from_numpy(b).cuda(), stream=ss.NoiseStream(K, 2)),
+                            mask.mask_rows(b, K, 2)):
+                assert np.array_equal(bits(g), nbits(w)), (K, N)
+    finally:
+        lib.efl_fxp_tune(25, -2)
+        lib.efl_fxp_tune(28, -2)

@@ -73,6 +73,26 @@ for _nb in (1, 2, 4):
     cases[f"dp_noise_elementwise_nb{_nb}"] = (8, _dp_blocks(_nb, 0))
 
 
+def _mask_shape(nb, st, fn):
+    def run():
+        lib.efl_fxp_tune(25, nb)
+        lib.efl_fxp_tune(28, st)
+        rc = fn()
+        lib.efl_fxp_tune(25, -2)       # back to the per-kernel defaults
+        lib.efl_fxp_tune(28, -2)
+        return rc
+    return run
+
+
+# efl_fxp_tune(25, nb) / (28, st): the secret-sharing mask kernels at 1 / 2 / 4 lane groups per
+# lane and plain / nontemporal / `nt sc1` stores (MASK_SWEEP=0 skips the sweep)
+if os.environ.get("MASK_SWEEP", "1") == "1":
+    for _name in ("noise", "share", "mask_cols", "mask_rows"):
+        for _nb in (1, 2, 4):
+            for _st in (0, 2, 7):
+                cases[f"{_name}_nb{_nb}_st{_st}"] = (cases[_name][0], _mask_shape(_nb, _st, cases[_name][1]))
+
+
 def cpu_sample(name, rows=1024):
     """The oracle (numpy, the reference's op chain) on the first `rows` rows; GiB/s of input."""
     from oracle import mask

@@ -6,7 +6,7 @@ HIP events per launch (medians over interleaved repetitions), for each of:
   plain        one table entry per slice (round 3's batched path)
   coalesced    adjacent slices merged into runs (one streaming launch when the batch is one run)
 and, for each, the fp32 batched tile shapes given in C3_SHAPES="name:enc_block,enc_k,dec_block,dec_k
-[,enc_order,dec_order];..." (efl_fxp_tune 10-13, 17-18). C3_LAYOUTS limits the layouts (default
+[,enc_order,dec_order[,enc_tiles,dec_tiles]];..." (efl_fxp_tune 10-13, 17-18, 26-27). C3_LAYOUTS limits the layouts (default
 "separate,views"). Prints one JSON line."""
 import json
 import os
@@ -57,7 +57,7 @@ def main():
         def run():
             if shape is None:
                 return fn()
-            kinds = (10, 11, 12, 13, 17, 18)[:len(shape)]
+            kinds = (10, 11, 12, 13, 17, 18, 26, 27)[:len(shape)]
             old = [lib.efl_fxp_tune(kind, v) for kind, v in zip(kinds, shape)]
             try:
                 return fn()

@@ -24,7 +24,8 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--order", type=int, nargs=2, default=None, help="efl_fxp_tune 17 / 18 (batched tile order)")
     ap.add_argument("--shapes", default="default;512,2,512,2",
-                    help="';'-separated batched shapes: 'default' or enc_block,enc_k,dec_block,dec_k (tune 10-13)")
+                    help="';'-separated batched shapes: 'default' or enc_block,enc_k,dec_block,dec_k[,enc_order,dec_order"
+                         "[,enc_tiles,dec_tiles]] (tune 10-13, 17-18, 26-27)")
     a = ap.parse_args()
     dev = efl.lib.require_gpu()
     lib = efl.lib.raw()
@@ -59,7 +60,8 @@ def main():
         shape = None if spec == "default" else [int(v) for v in spec.split(",")]
         old = None
         if shape:
-            old = [lib.efl_fxp_tune(kind, v) for kind, v in zip((10, 11, 12, 13), shape)]
+            kinds = (10, 11, 12, 13, 17, 18, 26, 27)[:len(shape)]
+            old = [lib.efl_fxp_tune(kind, v) for kind, v in zip(kinds, shape)]
             efl.lib.check(min(0, *old))
         torch._foreach_zero_(ys)
         for _ in range(3):
@@ -68,7 +70,7 @@ def main():
         ok = all(torch.equal(x, y) for x, y in zip(xs[::97], ys[::97]))
         arms[spec] = {"batched_step_ms": round(ms, 4), "roundtrip_ok": ok}
         if old:
-            for kind, v in zip((10, 11, 12, 13), old):
+            for kind, v in zip(kinds, old):
                 lib.efl_fxp_tune(kind, v)
     del Ms, Es, ys, enc_t, dec_t
     x = torch.randn(S * N, device=dev, generator=g)

@@ -43,6 +43,15 @@ run() {
               python3 tools/pmc_reduce.py gpurun_out/r06_c3_pmc$i --match batched k_stream --prune \
                 > gpurun_out/r06_c3_pmc$i.json || return $?
             done ;;
+    c3pmct) for i in ${C3PMC_PASSES:-3 1}; do
+              v="C3PMC_$i"
+              timeout -s KILL 120 rocprofv3 --pmc ${!v} --kernel-include-regex 'k_batched|k_stream' \
+                -d gpurun_out/r06_c3_pmct$i -o run --output-format csv \
+                -- python3 tools/config3_probe.py --reps 10 --shapes "default;512,1,512,2,0,0,1,2;512,1,512,2,0,0,1,4;512,1,512,2,0,0,2,1" \
+                > gpurun_out/r06_c3_pmct$i.log 2>&1 || return $?
+              python3 tools/pmc_reduce.py gpurun_out/r06_c3_pmct$i --match batched k_stream --prune \
+                > gpurun_out/r06_c3_pmct$i.json || return $?
+            done ;;
     stagep) timeout -k 10 1000 python -u bench.py --stage p > gpurun_out/r06_stage_p.jsonl 2> gpurun_out/r06_stage_p.err ;;
     stagepq) timeout -k 10 600 python -u bench.py --stage p --no-cpu-baseline > gpurun_out/r06_stage_pq.jsonl 2> gpurun_out/r06_stage_pq.err ;;
     profp)  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/r06_prof_p -o run --output-format csv \
@@ -54,6 +63,37 @@ run() {
               tests/test_crt_walks_gpu.py tests/test_walk_split_gpu.py > gpurun_out/r06_pltests.log 2>&1 ;;
     c3dec)  C3_LAYOUTS=separate C3_SHAPES="d1:512,1,512,1;d128:512,1,128,1;d256x4:512,1,256,4;d512x4:512,1,512,4;o1:512,1,512,2,0,1;o2:512,1,512,2,0,2;d128o2:512,1,128,1,0,2;e2:512,2,512,2;e2o2:512,2,512,2,2,0;e256:256,2,512,2" \
               timeout -k 10 300 python -u tools/config3_coalesce_probe.py >> gpurun_out/r06_c3_dec.jsonl 2> gpurun_out/r06_c3_dec.err ;;
+    c3t)    C3_LAYOUTS=separate C3_SHAPES="e1t2:512,1,512,2,0,0,2,1;e1t4:512,1,512,2,0,0,4,1;e1t8:512,1,512,2,0,0,8,1;d2t2:512,1,512,2,0,0,1,2;d2t4:512,1,512,2,0,0,1,4;d2t8:512,1,512,2,0,0,1,8;e2t4:512,2,512,2,0,0,4,1;d1t8:512,1,512,1,0,0,1,8;both4:512,1,512,2,0,0,4,4;both8:512,1,512,2,0,0,8,4" \
+              timeout -k 10 300 python -u tools/config3_coalesce_probe.py >> gpurun_out/r06_c3_tiles.jsonl 2> gpurun_out/r06_c3_tiles.err ;;
+    mask9)  timeout -k 10 400 python -u tools/bench_mask.py --rounds 9 --no-cpu-baseline > gpurun_out/r06_bench_mask9.jsonl 2> gpurun_out/r06_bench_mask9.err ;;
+    crtt)   timeout -k 10 900 $PT tests/test_crt_walks_gpu.py tests/test_walk_split_gpu.py tests/test_paillier_crt_gpu.py \
+              tests/test_ctx_abi_gpu.py > gpurun_out/r06_crt_tests.log 2>&1 ;;
+    decab)  for r in 1 2; do
+              for v in "" _nofold; do
+                EFL_HIP_LIB=$LIBDIR/libefl_hip$v.so timeout -k 10 300 python -u tools/dec_ab.py --label "lib$v" \
+                  >> gpurun_out/r06_dec_ab.jsonl 2>> gpurun_out/r06_dec_ab.err || return $?
+              done
+            done ;;
+    dect)   timeout -k 10 900 $PT tests/test_paillier_gpu.py tests/test_paillier_key_sizes_gpu.py -k "decrypt or round_trip" \
+              > gpurun_out/r06_dec_tests.log 2>&1 ;;
+    decpmc) for v in _fold _nofold; do
+              EFL_HIP_LIB=$LIBDIR/libefl_hip$v.so timeout -s KILL 150 rocprofv3 \
+                --pmc SQC_ICACHE_MISSES SQC_ICACHE_HITS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_WAVES \
+                --kernel-include-regex 'k_decrypt' -d gpurun_out/r06_dec_pmc$v -o run --output-format csv \
+                -- python3 tools/dec_ab.py --reps 1 --label "lib$v" > gpurun_out/r06_dec_pmc$v.log 2>&1 || return $?
+              python3 tools/pmc_reduce.py gpurun_out/r06_dec_pmc$v --match k_decrypt > gpurun_out/r06_dec_pmc$v.json || return $?
+            done ;;
+    maskpmc) for c in FETCH_SIZE WRITE_SIZE; do
+              MASK_SWEEP=0 timeout -s KILL 150 rocprofv3 --pmc $c --kernel-include-regex 'k_mask|k_noise' \
+                -d gpurun_out/r06_mask_pmc_$c -o run --output-format csv \
+                -- python3 tools/bench_mask.py --steps 5 --rounds 1 --no-cpu-baseline > gpurun_out/r06_mask_pmc_$c.log 2>&1 || return $?
+              python3 tools/pmc_reduce.py gpurun_out/r06_mask_pmc_$c --match k_mask k_noise --prune \
+                > gpurun_out/r06_mask_pmc_$c.json || return $?
+            done ;;
+    masklay) timeout -k 10 300 python -u tools/mask_layout_probe.py >> gpurun_out/r06_mask_layout.jsonl 2> gpurun_out/r06_mask_layout.err ;;
+    crtprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r06_crt_prof -o run --output-format csv \
+              -- python3 tools/crt_tail_ab.py --modes 1,16,8 --rounds 2 > gpurun_out/r06_crt_prof.log 2>&1 ;;
+    crtab)  timeout -k 10 400 python -u tools/crt_tail_ab.py >> gpurun_out/r06_crt_tail_ab.jsonl 2> gpurun_out/r06_crt_tail_ab.err ;;
     ab)     timeout -k 10 300 python -u tools/ab_fxp_libs.py r05=$LIBDIR/libefl_hip_r05.so cur=$LIBDIR/libefl_hip.so \
               pre=$LIBDIR/libefl_hip_pre.so >> gpurun_out/r06_ab_libs.jsonl 2> gpurun_out/r06_ab_libs.err ;;
     *) echo "unknown step $1"; return 2 ;;
