@@ -754,6 +754,8 @@ std::atomic<int> g_dp_blocks{4};
 // 0.67
 std::atomic<int> g_mask_blocks[4] = {{2}, {1}, {1}, {1}};
 std::atomic<int> g_mask_store[4] = {{0}, {7}, {2}, {7}};
+std::atomic<int> g_rows_half{1};
+std::atomic<int> g_noise_half{1};
 }  // namespace efl
 
 EFL_API int efl_fxp_tune(int kind, int value) {
@@ -799,6 +801,12 @@ EFL_API int efl_fxp_tune(int kind, int value) {
   if (kind == 16) {                 // streaming fp32 encode: exponent stores first
     if (value != 0 && value != 1) return EFL_E_INVALID_ARGUMENT;
     return g_e_first.exchange(value);
+  }
+  if (kind == 29 || kind == 30) {   // mask_rows / share + weight noise: one lane (0) or wave halves (1)
+    std::atomic<int>& v = kind == 29 ? g_rows_half : g_noise_half;
+    if (value == -1) return v.load();
+    if (value != 0 && value != 1) return EFL_E_INVALID_ARGUMENT;
+    return v.exchange(value);
   }
   if (kind == 26 || kind == 27) {   // batched fp32 encode / decode: tiles per workgroup
     std::atomic<int>& v = g_batch_tiles[kind - 26];

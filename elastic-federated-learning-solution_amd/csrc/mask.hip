@@ -525,8 +525,96 @@ void group_magic(long long total, long long d, uint32_t* m, int* sh) {
   *m = (uint32_t)(((1ull << (31 + l)) / (unsigned long long)d) + 1ull);
   *sh = 31 + l;
 }
+// share / weight noise (op 1 / 2) with the two outputs over the two halves of a wave
+// (efl_fxp_tune(30, 1), the default since round 6): lanes l and l + 32 load the same 16-byte group
+// (one HBM read; the second half's request hits the line the first fetched), draw the same Philox
+// block, and store o0 (l < 32) or o1 (l >= 32): one load and one store per lane, as mask_rows'
+// halves. 0.72 -> 0.75 of 8 TB/s on two boxes.
+template <int OP, int DIV, int ST>
+__global__ __launch_bounds__(kBlock) void k_noise_half(const float* __restrict__ x, float* __restrict__ o0,
+                                                       float* __restrict__ o1, long long n, uint64_t seed,
+                                                       uint64_t ctr0, float d) {
+  const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
+  const int half = (int)((threadIdx.x >> 5) & 1);
+  const long long g = (t >> 6) * 32 + (threadIdx.x & 31), i0 = g * 4;
+  if (i0 >= n) return;
+  float* o = half ? o1 : o0;
+  float u[4];
+  draw4(seed, ctr0 + (uint64_t)g, u);
+  if (i0 + 4 <= n) {
+    const f4 v = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + g);
+    f4 a, c;
+    noise_f4<OP, DIV>(v, u, d, a, c);
+    stv<ST>(reinterpret_cast<f4*>(o) + g, half ? c : a);
+    return;
+  }
+  for (int j = 0; j < 4 && i0 + j < n; ++j) {
+    const float xv = x[i0 + j];
+    const float nz = noise<DIV>(u[j], xv, d);
+    if (OP == 1) o[i0 + j] = half ? xv - nz : nz;
+    if (OP == 2) o[i0 + j] = half ? xv + nz : xv - nz;
+  }
+}
+
+// Mode B with the row pair split over the two halves of a wave (efl_fxp_tune(29, 1), the default
+// since round 6): lane l < 32 owns row 2j, lane l + 32 row 2j + 1 of the same four columns, so a lane
+// loads one 16-byte group and stores three (its send and keep0 rows, then the send difference row
+// from the even half or the keep sum row from the odd half, f swapped between the halves). A wave
+// owns NB runs of 32 groups (kind 25): all NB loads first, the NB Philox chains together. Same values
+// and Philox blocks as k_mask_rows; 0.66 -> 0.78 of 8 TB/s at [65536, 1024].
+template <int NB, int ST>
+__global__ __launch_bounds__(kBlock) void k_mask_rows_half(const float* __restrict__ b, float* __restrict__ send,
+                                                           float* __restrict__ keep0, float* __restrict__ keep1,
+                                                           long long K, long long N, uint64_t seed, uint64_t ctr0,
+                                                           uint32_t dm, int ds) {
+  const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
+  const int l = (int)(threadIdx.x & 63), half = l >> 5;
+  const long long g0 = (t >> 6) * (32 * NB) + (l & 31);
+  const long long nq = N / 4, total = (K / 2) * nq;
+  long long i[NB], o[NB];
+  bool valid[NB];
+  f4 x[NB];
+  uint64_t blk[NB];
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    const long long g = g0 + 32 * k;
+    valid[k] = g < total;
+    const long long gv = valid[k] ? g : 0;
+    const long long j = div_groups(gv, nq, dm, ds), q = gv - j * nq;
+    i[k] = (2 * j + half) * N + 4 * q;
+    o[k] = half == 0 ? K * N + j * N + 4 * q : j * N + 4 * q;   // send difference row / keep sum row
+    x[k] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    if (valid[k]) x[k] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(b + i[k]));
+    blk[k] = ctr0 + (uint64_t)(i[k] >> 2);
+  }
+  float u[NB][4];
+  uniforms<NB>(seed, blk, u);
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    float f[4], pf[4];
+    f4 sv, kv, dv;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      f[c] = u[k][c] * x[k][c];
+      const float h = x[k][c] / 2.0f;
+      sv[c] = h - f[c];
+      kv[c] = h + f[c];
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) pf[c] = __shfl_xor(f[c], 32);   // every lane takes part
+#pragma unroll
+    for (int c = 0; c < 4; ++c) dv[c] = half == 0 ? f[c] - pf[c] : f[c] + pf[c];   // fe - fo ; fo + fe
+    if (valid[k]) {
+      stv<ST>(reinterpret_cast<f4*>(send + i[k]), sv);
+      stv<ST>(reinterpret_cast<f4*>(keep0 + i[k]), kv);
+      stv<ST>(reinterpret_cast<f4*>((half == 0 ? send : keep1) + o[k]), dv);
+    }
+  }
+}
+
 #define EFL_K_COLS4(NB, ST) k_mask_cols4<NB, ST>
 #define EFL_K_ROWS4(NB, ST) k_mask_rows<4, NB, ST>
+#define EFL_K_ROWSH(NB, ST) k_mask_rows_half<NB, ST>
 
 }  // namespace
 
@@ -535,6 +623,8 @@ void group_magic(long long total, long long d, uint32_t* m, int* sh) {
 extern std::atomic<int> g_dp_blocks;
 extern std::atomic<int> g_mask_blocks[4];   // [noise, share / weight noise, mask_cols, mask_rows]
 extern std::atomic<int> g_mask_store[4];
+extern std::atomic<int> g_noise_half;       // efl_fxp_tune(30, v): share / weight noise over wave halves (1, default)
+extern std::atomic<int> g_rows_half;        // efl_fxp_tune(29, v): mode B over wave halves (1, default) or not (0)
 
 }  // namespace efl
 
@@ -561,6 +651,17 @@ EFL_API int efl_ss_noise(const float* x, float* out0, float* out1, int64_t n, in
                     std::isnormal(1.0f / divisor);
   const int dv = divisor == 1.0f ? 0 : pow2 ? 1 : 2;
   const float d = dv == 1 ? 1.0f / divisor : divisor;
+  if (op != 0 && g_noise_half.load(std::memory_order_relaxed)) {
+    const unsigned grid = (unsigned)(((lanes + 31) / 32 * 64 + kBlock - 1) / kBlock);
+    const int st = g_mask_store[1].load(std::memory_order_relaxed);
+#define EFL_NH(OP, DV) \
+    (st == 7 ? k_noise_half<OP, DV, 7> : st == 2 ? k_noise_half<OP, DV, 2> : k_noise_half<OP, DV, 0>)
+    auto* kern = op == 1 ? (dv == 0 ? EFL_NH(1, 0) : dv == 1 ? EFL_NH(1, 1) : EFL_NH(1, 2))
+                         : (dv == 0 ? EFL_NH(2, 0) : dv == 1 ? EFL_NH(2, 1) : EFL_NH(2, 2));
+#undef EFL_NH
+    kern<<<grid, kBlock, 0, s>>>(x, out0, out1, n, seed, ctr0, d);
+    return hip_status(hipGetLastError(), "efl_ss_noise");
+  }
   const int fam = op == 0 ? 0 : 1;
   const int nb = g_mask_blocks[fam].load(std::memory_order_relaxed);
   const int st = g_mask_store[fam].load(std::memory_order_relaxed);
@@ -618,7 +719,13 @@ EFL_API int efl_ss_mask_rows(const float* b, float* send, float* keep0, float* k
   uint32_t dm;
   int ds;
   group_magic(lanes, v4 ? cols / 4 : cols, &dm, &ds);
-  if (v4)
+  if (v4 && g_rows_half.load(std::memory_order_relaxed)) {
+    // a wave per 32 NB lane groups: (waves x 64) threads
+    const int nb = g_mask_blocks[3].load(std::memory_order_relaxed);
+    const long long waves = (lanes + 32 * nb - 1) / (32 * nb);
+    EFL_MASK_LAUNCH(nb, g_mask_store[3].load(std::memory_order_relaxed), waves * 64 * nb, s, EFL_K_ROWSH, b, send,
+                    keep0, keep1, rows, cols, seed, ctr0, dm, ds);
+  } else if (v4)
     EFL_MASK_LAUNCH(g_mask_blocks[3].load(std::memory_order_relaxed), g_mask_store[3].load(std::memory_order_relaxed),
                     lanes, s, EFL_K_ROWS4, b, send, keep0, keep1, rows, cols, seed, ctr0, dm, ds);
   else k_mask_rows<1, 1, 0><<<grid_for(lanes), kBlock, 0, s>>>(b, send, keep0, keep1, rows, cols, seed, ctr0, dm, ds);

@@ -84,7 +84,10 @@ const char* efl_last_error(void);
  * efl_ss_mask_rows (1, 2, 4), kind 28 their store flavour (0 plain, 2 nontemporal, 7 `nt sc1`): each
  * has a per-kernel default; setting a value sets all kernels, -2 restores the defaults; kinds 26 / 27
  * = tiles per workgroup of the batched encode / decode (1, 2, 4, 8). Batched tile defaults (kinds 10-13): encode 512 lanes x 1 pair,
- * decode 512 x 2. Value -1 on kinds 10-13, 20 and 25 reads the current value without changing it.
+ * decode 512 x 2. Kind 29 = efl_ss_mask_rows with the row pair over the two halves of a wave (1,
+ * default) or in one lane (0, round 5's kernel); kind 30 the same for the two outputs of
+ * efl_ss_noise ops 1 and 2 (1 over the wave halves, default; 0 both in one lane). Value -1 on kinds
+ * 10-13, 20, 25, 29 and 30 reads the current value without changing it.
  * Returns the previous value or EFL_E_INVALID_ARGUMENT. */
 int efl_fxp_tune(int kind, int value);
 

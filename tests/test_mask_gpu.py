@@ -160,3 +160,53 @@ def test_mask_variants_identical(ss, nb, st):
     finally:
         lib.efl_fxp_tune(25, -2)
         lib.efl_fxp_tune(28, -2)
+
+
+@pytest.mark.parametrize("half", [0, 1])
+@pytest.mark.parametrize("nb", [1, 2, 4])
+@pytest.mark.parametrize("st", [0, 2, 7])
+def test_mask_rows_layouts_identical(ss, half, nb, st):
+    """mask_rows with the row pair over the halves of a wave (efl_fxp_tune 29 = 1, the default) and in
+    one lane (0), at every lane-group count and store flavour, gives the oracle's bits: one lane
+    group, partial waves (33 groups a row pair), and full ones."""
+    import efl
+    lib = efl.lib.raw()
+    assert lib.efl_fxp_tune(29, -1) == 1                       # the halves by default
+    assert lib.efl_fxp_tune(29, 2) < 0
+    lib.efl_fxp_tune(29, half)
+    lib.efl_fxp_tune(25, nb)
+    lib.efl_fxp_tune(28, st)
+    try:
+        for K, N in ((2, 4), (6, 132), (514, 1024), (392, 256), (130, 4 * 33 * 3)):
+            b = rand((K, N), K * 7 + N)
+            for g, w in zip(ss.mask_rows(torch.from_numpy(b).cuda(), stream=ss.NoiseStream(K, 2)),
+                            mask.mask_rows(b, K, 2)):
+                assert np.array_equal(bits(g), nbits(w)), (K, N)
+    finally:
+        lib.efl_fxp_tune(29, 1)
+        lib.efl_fxp_tune(25, -2)
+        lib.efl_fxp_tune(28, -2)
+
+
+@pytest.mark.parametrize("half", [0, 1])
+@pytest.mark.parametrize("st", [0, 2, 7])
+def test_noise_halves_identical(ss, half, st):
+    """share and weight noise with the two outputs over the halves of a wave (efl_fxp_tune 30 = 1, the
+    default) and both in one lane (0) give the oracle's bits, at sizes ending in a partial group, a partial wave, and full waves."""
+    import efl
+    lib = efl.lib.raw()
+    assert lib.efl_fxp_tune(30, -1) == 1                       # the halves by default
+    assert lib.efl_fxp_tune(30, 2) < 0
+    prev = lib.efl_fxp_tune(30, half)
+    lib.efl_fxp_tune(28, st)
+    try:
+        for n in (5, 4 * 33 + 2, 4096 * 4 + 12, 4 * 256 * 4 * 3 + 4):
+            x = rand(n, n + 3)
+            for op, div in ((1, 1.0), (2, 3.0), (1, 4.0)):
+                got = ss._noise(torch.from_numpy(x).cuda(), op, div, stream=ss.NoiseStream(n, 9))
+                want = mask.noise(x, n, 9, op, div)
+                for g, w in zip(got, want):
+                    assert np.array_equal(bits(g), nbits(w)), (n, op, div)
+    finally:
+        lib.efl_fxp_tune(30, prev)
+        lib.efl_fxp_tune(28, -2)

@@ -93,6 +93,48 @@ if os.environ.get("MASK_SWEEP", "1") == "1":
                 cases[f"{_name}_nb{_nb}_st{_st}"] = (cases[_name][0], _mask_shape(_nb, _st, cases[_name][1]))
 
 
+def _rows_layout(half, nb, st, fn):
+    """efl_fxp_tune(29, half): mask_rows with the row pair over the two halves of a wave (1, the
+    default) or in one lane (0, round 5's kernel), at nb lane groups per lane and store flavour st"""
+    def run():
+        lib.efl_fxp_tune(29, half)
+        lib.efl_fxp_tune(25, nb)
+        lib.efl_fxp_tune(28, st)
+        rc = fn()
+        lib.efl_fxp_tune(29, 1)
+        lib.efl_fxp_tune(25, -2)
+        lib.efl_fxp_tune(28, -2)
+        return rc
+    return run
+
+
+cases["mask_rows_pair"] = (16, _rows_layout(0, 1, 7, cases["mask_rows"][1]))
+
+
+def _noise_halves(half, st, fn):
+    """efl_fxp_tune(30, half): share / weight noise with the outputs over the halves of a wave"""
+    def run():
+        lib.efl_fxp_tune(30, half)
+        lib.efl_fxp_tune(28, st)
+        rc = fn()
+        lib.efl_fxp_tune(30, 1)
+        lib.efl_fxp_tune(28, -2)
+        return rc
+    return run
+
+
+cases["share_one_lane"] = (12, _noise_halves(0, 7, cases["share"][1]))
+cases["weight_noise_one_lane"] = (12, _noise_halves(0, 7, cases["weight_noise"][1]))
+if os.environ.get("MASK_SWEEP", "1") == "1":
+    for _st in (0, 2, 7):
+        cases[f"share_half_st{_st}"] = (12, _noise_halves(1, _st, cases["share"][1]))
+        cases[f"weight_noise_half_st{_st}"] = (12, _noise_halves(1, _st, cases["weight_noise"][1]))
+if os.environ.get("MASK_SWEEP", "1") == "1" or os.environ.get("MASK_ROWS_SWEEP") == "1":
+    for _nb in (1, 2, 4):
+        for _st in (0, 2, 7):
+            cases[f"mask_rows_half_nb{_nb}_st{_st}"] = (16, _rows_layout(1, _nb, _st, cases["mask_rows"][1]))
+
+
 def cpu_sample(name, rows=1024):
     """The oracle (numpy, the reference's op chain) on the first `rows` rows; GiB/s of input."""
     from oracle import mask

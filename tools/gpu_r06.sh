@@ -83,6 +83,8 @@ run() {
                 -- python3 tools/dec_ab.py --reps 1 --label "lib$v" > gpurun_out/r06_dec_pmc$v.log 2>&1 || return $?
               python3 tools/pmc_reduce.py gpurun_out/r06_dec_pmc$v --match k_decrypt > gpurun_out/r06_dec_pmc$v.json || return $?
             done ;;
+    traffic) python3 tools/pmc_traffic.py gpurun_out/r06_prof_fetch/run_counter_collection.csv \
+              gpurun_out/r06_prof_write/run_counter_collection.csv 67108864 profiles/r06 > gpurun_out/r06_pmc_traffic.json ;;
     maskpmc) for c in FETCH_SIZE WRITE_SIZE; do
               MASK_SWEEP=0 timeout -s KILL 150 rocprofv3 --pmc $c --kernel-include-regex 'k_mask|k_noise' \
                 -d gpurun_out/r06_mask_pmc_$c -o run --output-format csv \
@@ -90,7 +92,7 @@ run() {
               python3 tools/pmc_reduce.py gpurun_out/r06_mask_pmc_$c --match k_mask k_noise --prune \
                 > gpurun_out/r06_mask_pmc_$c.json || return $?
             done ;;
-    masklay) timeout -k 10 300 python -u tools/mask_layout_probe.py >> gpurun_out/r06_mask_layout.jsonl 2> gpurun_out/r06_mask_layout.err ;;
+    masklay) timeout -k 10 300 python -u tools/mask_layout_probe.py ${MASKLAY_ARGS:-} >> gpurun_out/r06_mask_layout.jsonl 2> gpurun_out/r06_mask_layout.err ;;
     crtprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r06_crt_prof -o run --output-format csv \
               -- python3 tools/crt_tail_ab.py --modes 1,16,8 --rounds 2 > gpurun_out/r06_crt_prof.log 2>&1 ;;
     crtab)  timeout -k 10 400 python -u tools/crt_tail_ab.py >> gpurun_out/r06_crt_tail_ab.jsonl 2> gpurun_out/r06_crt_tail_ab.err ;;
