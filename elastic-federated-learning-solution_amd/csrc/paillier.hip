@@ -1450,11 +1450,11 @@ EFL_API int efl_pl_tune(int ln, int decrypt, int limbs_per_lane) {
     if (limbs_per_lane > 2) { set_error("CRT walk mode must be 0 (chosen), 1 (per key) or 2 (paired lanes)"); return EFL_E_INVALID_ARGUMENT; }
     return pl::sl_crt_fused(limbs_per_lane);
   }
-  if (decrypt == 6) {   // the paired CRT encryption's tail: 0 / 1 split + join, 2/4/8/16 tree S
+  if (decrypt == 6) {   // the paired CRT encryption's tail: 0 mixed launch, 1 split + join, 2/4/8/16 tree S
     if (limbs_per_lane < 0) return pl::sl_crt_tail(-1);
     if (limbs_per_lane != 0 && limbs_per_lane != 1 && limbs_per_lane != 2 && limbs_per_lane != 4 &&
         limbs_per_lane != 8 && limbs_per_lane != 16) {
-      set_error("CRT tail mode must be 0 or 1 (split and join) or 2, 4, 8, 16 (tree parts)");
+      set_error("CRT tail mode must be 0 (tree waves in the whole launch), 1 (split and join) or 2, 4, 8, 16 (tree parts)");
       return EFL_E_INVALID_ARGUMENT;
     }
     return pl::sl_crt_tail(limbs_per_lane);

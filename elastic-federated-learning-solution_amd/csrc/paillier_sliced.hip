@@ -1934,15 +1934,16 @@ __device__ __forceinline__ bool pair_lane(long long w, long long N, long long& e
   return el < N;
 }
 
+// wave w of the whole rounds: lanes 0-31 the p halves, 32-63 the q halves of elements 32 w ..
 template <int C>
-__global__ __launch_bounds__(kSlBlock, EFL_WALK1_WAVES) void k_crt_pair_whole(
-    Key kp, Key kq, const uint32_t* __restrict__ n2w, const long long* __restrict__ m,
-    const uint32_t* __restrict__ a_in, uint32_t* __restrict__ out, long long N, uint64_t seed, long long ctr0) {
+__device__ __forceinline__ void crt_pair_whole_wave(long long w, const Key& kp, const Key& kq,
+                                                    const uint32_t* __restrict__ n2w, const long long* __restrict__ m,
+                                                    const uint32_t* __restrict__ a_in, uint32_t* __restrict__ out,
+                                                    long long N, uint64_t seed, long long ctr0, uint32_t* lds) {
   constexpr int E = kSlBlock, C28 = s28::limbs_per_lane(C, 1);
-  extern __shared__ uint32_t lds[];
   long long el;
   bool q;
-  const bool valid = pair_lane<C>(blockIdx.x, N, el, q);
+  const bool valid = pair_lane<C>(w, N, el, q);
   const Key k = q ? kq : kp;
   uint32_t h[C];
   if (valid) {
@@ -1950,7 +1951,7 @@ __global__ __launch_bounds__(kSlBlock, EFL_WALK1_WAVES) void k_crt_pair_whole(
     uint32_t* B = lds + threadIdx.x;
     uint32_t* A = lds + C28 * E + threadIdx.x;
     if (a_in) {
-      for (int w = 0; w < words; ++w) A[w * E] = a_in[el * words + w];
+      for (int wd = 0; wd < words; ++wd) A[wd * E] = a_in[el * words + wd];
     } else {
       draw_a<1>(A, E, words, k.d.a_bits, seed, (uint64_t)(ctr0 + el), 0);
     }
@@ -1968,6 +1969,14 @@ __global__ __launch_bounds__(kSlBlock, EFL_WALK1_WAVES) void k_crt_pair_whole(
   lds_sync();
   const uint32_t* ox2 = q ? kp.at(kp.d.off_n2) : kq.at(kq.d.off_n2);   // the other prime's square
   pair_join<C>(h, ox2, n2w, lds, out + el * 2 * C, q, valid);
+}
+
+template <int C>
+__global__ __launch_bounds__(kSlBlock, EFL_WALK1_WAVES) void k_crt_pair_whole(
+    Key kp, Key kq, const uint32_t* __restrict__ n2w, const long long* __restrict__ m,
+    const uint32_t* __restrict__ a_in, uint32_t* __restrict__ out, long long N, uint64_t seed, long long ctr0) {
+  extern __shared__ uint32_t lds[];
+  crt_pair_whole_wave<C>(blockIdx.x, kp, kq, n2w, m, a_in, out, N, seed, ctr0, lds);
 }
 
 // part `part` of tail wave t (global wave w0 + t): slot v = (part * tw + t) * 64 + lane
@@ -2055,17 +2064,17 @@ __global__ __launch_bounds__(kSlBlock, EFL_WALK1_WAVES) void k_crt_pair_tjoin(
 // Lanes diverge only in the walk's trip count (rows differ by at most one) and in part 0's
 // lane_gstart; lds_sync is a wavefront fence, so the divergent calls are safe.
 template <int C, int S>
-__global__ __launch_bounds__(kSlBlock, EFL_WALK1_WAVES) void k_crt_pair_tree(
-    Key kp, Key kq, const uint32_t* __restrict__ n2w, const long long* __restrict__ m,
-    const uint32_t* __restrict__ a_in, uint32_t* __restrict__ out, long long N, long long el0, uint64_t seed,
-    long long ctr0) {
+__device__ __forceinline__ void crt_pair_tree_wave(long long wb, const Key& kp, const Key& kq,
+                                                   const uint32_t* __restrict__ n2w, const long long* __restrict__ m,
+                                                   const uint32_t* __restrict__ a_in, uint32_t* __restrict__ out,
+                                                   long long N, long long el0, uint64_t seed, long long ctr0,
+                                                   uint32_t* lds) {
   static_assert(S >= 2 && S <= 32 && (S & (S - 1)) == 0, "parts per element-half: a power of two dividing 32");
   constexpr int E = kSlBlock, C28 = s28::limbs_per_lane(C, 1);
-  extern __shared__ uint32_t lds[];
   const int lane = (int)threadIdx.x;
   const bool q = lane >= 32;
   const int part = lane % S;
-  const long long el = el0 + (long long)blockIdx.x * (32 / S) + (lane & 31) / S;
+  const long long el = el0 + wb * (32 / S) + (lane & 31) / S;
   const bool live = el < N;
   const Key k = q ? kq : kp;
   uint32_t* B = lds + lane;
@@ -2124,10 +2133,37 @@ __global__ __launch_bounds__(kSlBlock, EFL_WALK1_WAVES) void k_crt_pair_tree(
   pair_join<C>(h, ox2, n2w, lds, out + (valid ? el : 0) * 2 * C, q, valid);
 }
 
-// efl_pl_tune(ln, 6, v): the tail of the paired CRT encryption: 0 / 1 = the split-and-join launches
-// (round 5; tail_parts chooses the parts, 1 when the tail is not worth splitting), 2 / 4 / 8 / 16 = the
-// product tree across lanes with that S (round 6: bit-identical, measured no faster at the MNIST shape,
-// DESIGN.md §6a, so not the default)
+template <int C, int S>
+__global__ __launch_bounds__(kSlBlock, EFL_WALK1_WAVES) void k_crt_pair_tree(
+    Key kp, Key kq, const uint32_t* __restrict__ n2w, const long long* __restrict__ m,
+    const uint32_t* __restrict__ a_in, uint32_t* __restrict__ out, long long N, long long el0, uint64_t seed,
+    long long ctr0) {
+  extern __shared__ uint32_t lds[];
+  crt_pair_tree_wave<C, S>(blockIdx.x, kp, kq, n2w, m, a_in, out, N, el0, seed, ctr0, lds);
+}
+
+// The tail's tree waves and the whole rounds in ONE launch, the tree waves first (round 6, tail mode
+// 0). Launched apart, the tail ran after the whole rounds, one wave per SIMD at most and latency
+// bound (about 0.6 of a whole wave's time for 2 % of the work). Here blocks [0, tb) are tree waves of
+// elements el0 .. N - 1 and blocks tb .. are whole waves 0 .. of elements 0 .. el0 - 1: each SIMD
+// takes a short tree wave beside its first whole wave, and the dispatcher fills the slots the tree
+// waves free with whole waves, so the tail's work spreads over the whole launch.
+template <int C, int S>
+__global__ __launch_bounds__(kSlBlock, EFL_WALK1_WAVES) void k_crt_pair_mixed(
+    Key kp, Key kq, const uint32_t* __restrict__ n2w, const long long* __restrict__ m,
+    const uint32_t* __restrict__ a_in, uint32_t* __restrict__ out, long long N, long long el0, long long tb,
+    uint64_t seed, long long ctr0) {
+  extern __shared__ uint32_t lds[];
+  const long long b = blockIdx.x;
+  if (b < tb) crt_pair_tree_wave<C, S>(b, kp, kq, n2w, m, a_in, out, N, el0, seed, ctr0, lds);
+  else crt_pair_whole_wave<C>(b - tb, kp, kq, n2w, m, a_in, out, el0, seed, ctr0, lds);
+}
+
+// efl_pl_tune(ln, 6, v): the tail of the paired CRT encryption: 0 = the tail's tree waves in the same
+// launch as the whole rounds, ahead of them (k_crt_pair_mixed, S chosen per launch; round 6), 1 = the
+// split-and-join launches (round 5; tail_parts chooses the parts, 1 when the tail is not worth
+// splitting), 2 / 4 / 8 / 16 = the product tree with that S as a launch of its own after the whole
+// rounds (round 6: no faster than 1 at the MNIST shape)
 std::atomic<int> g_crt_tail{0};
 
 // efl_pl_tune(ln, 5, v): the key owner's CRT encryption, 0 = chosen per launch (the paired lanes
@@ -2165,9 +2201,39 @@ hipError_t run_crt_pair(const Key& kp, const Key& kq, const uint32_t* n2w, const
   const long long waves = (N + 31) / 32;
   long long whole = 0;
   double cost = 0.0;
-  const int S = g_crt_tail.load(std::memory_order_relaxed);   // >= 2: the tree tail with S parts
+  const int mode = g_crt_tail.load(std::memory_order_relaxed);
+  int S = mode;                        // >= 2: the tree tail with S parts, launched after the whole rounds
   const bool tree = S >= 2;
   int parts = 1;
+  if (mode == 0) {
+    // the largest S <= 16 whose tree waves (tail elements x S / 32) still fit one per SIMD; none: the
+    // tail runs as plain whole waves
+    whole = waves / simd_count() * simd_count();
+    const long long tail_el = N - whole * 32;
+    S = 1;
+    for (int P = 2; P <= 16; P <<= 1)
+      if (tail_el > 0 && (tail_el * P + 31) / 32 <= simd_count()) S = P;
+    const size_t walk_lds0 = (size_t)(C28 + (kp.d.a_bits + 31) / 32) * E * 4, join_lds0 = (size_t)(2 * C + 1) * 32 * 4;
+    const size_t lds0 = walk_lds0 > join_lds0 ? walk_lds0 : join_lds0;
+    if (S == 1) {
+      hipLaunchKernelGGL((k_crt_pair_whole<C>), dim3((unsigned)waves), dim3(kSlBlock), lds0, s, kp, kq, n2w, m, a, out,
+                         N, seed, ctr0);
+      return hipGetLastError();
+    }
+    const long long el0 = whole * 32, tb = (tail_el * S + 31) / 32;
+    const unsigned grid = (unsigned)(tb + whole);
+    switch (S) {
+      case 2: hipLaunchKernelGGL((k_crt_pair_mixed<C, 2>), dim3(grid), dim3(kSlBlock), lds0, s, kp, kq, n2w, m, a, out,
+                                 N, el0, tb, seed, ctr0); break;
+      case 4: hipLaunchKernelGGL((k_crt_pair_mixed<C, 4>), dim3(grid), dim3(kSlBlock), lds0, s, kp, kq, n2w, m, a, out,
+                                 N, el0, tb, seed, ctr0); break;
+      case 8: hipLaunchKernelGGL((k_crt_pair_mixed<C, 8>), dim3(grid), dim3(kSlBlock), lds0, s, kp, kq, n2w, m, a, out,
+                                 N, el0, tb, seed, ctr0); break;
+      default: hipLaunchKernelGGL((k_crt_pair_mixed<C, 16>), dim3(grid), dim3(kSlBlock), lds0, s, kp, kq, n2w, m, a,
+                                  out, N, el0, tb, seed, ctr0); break;
+    }
+    return hipGetLastError();
+  }
   if (tree) {
     whole = waves / simd_count() * simd_count();   // the whole rounds; the rest is the tree tail
   } else {

@@ -119,10 +119,11 @@ def test_extreme_plaintexts(efl, owner):
 
 
 @pytest.mark.parametrize("tail", [0, 1, 2, 4, 8, 16])
-@pytest.mark.parametrize("n", [1, 17, 65, 2048, 100352, 100352 + 5 * 64 + 3])
+@pytest.mark.parametrize("n", [1, 17, 65, 2048, 32769, 100352, 100352 + 5 * 64 + 3])
 def test_tree_tail_equals_per_key(efl, owner, tail, n):
-    """The tail past the whole rounds as a product tree across lanes (efl_pl_tune(ln, 6, v): 2-16 a
-    fixed S) or as the round-5 split-and-join launches (0, the default, and 1): ciphertexts and
+    """The tail past the whole rounds as a product tree across lanes, in the whole rounds' launch
+    (efl_pl_tune(ln, 6, 0), the default) or after it (2-16, a fixed S), or as the round-5
+    split-and-join launches (1): ciphertexts and
     hs^(a') equal the per-key walks' bit for bit, for tails of every size (a lone element, a part-empty
     wave, the MNIST activation's 2,048 elements, and a count whose tail is neither)."""
     lib = efl.lib.raw()
@@ -142,5 +143,5 @@ def test_tree_tail_equals_per_key(efl, owner, tail, n):
 
 def test_tree_tail_knob(efl):
     lib = efl.lib.raw()
-    assert lib.efl_pl_tune(16, 6, -1) == 0               # split and join by default; the tree on request
+    assert lib.efl_pl_tune(16, 6, -1) == 0               # the tree waves inside the whole launch by default
     assert lib.efl_pl_tune(16, 6, 3) < 0 and lib.efl_pl_tune(16, 6, 32) < 0

@@ -182,6 +182,7 @@ for name, (bpe, fn) in cases.items():
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbs / PEAK_GBS, 4), "bytes_per_elem": bpe},
             "library": efl.lib.version()}
-    if not args.no_cpu_baseline and "_nb" not in name:
+    if not args.no_cpu_baseline and name in ("noise", "share", "weight_noise", "mask_cols", "mask_rows",
+                                             "dp_noise_elementwise", "dp_noise_gaussian"):
         line["cpu_baseline"] = cpu_sample(name)
     print(json.dumps(line), flush=True)
