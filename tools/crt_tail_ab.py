@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--modes", default="1,0,16,8")
+    ap.add_argument("--shapes", default="100352,100675,50176")
     a = ap.parse_args()
     import efl
     from efl.privacy import paillier_cipher as pc
@@ -40,7 +41,7 @@ def main():
     modes = [int(v) for v in a.modes.split(",")]
     out = {"tool": "crt_tail_ab", "library": efl.lib.version(), "reps": a.reps, "rounds": a.rounds, "shapes": {}}
     prev = lib.efl_pl_tune(16, 6, -1)
-    for N in (100352, 100352 + 5 * 64 + 3, 50176):
+    for N in (int(v) for v in a.shapes.split(",")):
         g = torch.Generator(device=dev).manual_seed(N)
         m = torch.randint(-2**40, 2**40, (N,), dtype=torch.int64, device=dev, generator=g)
         cts = {v: torch.empty((N, k.lc), dtype=torch.int32, device=dev) for v in modes}

@@ -52,7 +52,7 @@ run() {
               python3 tools/pmc_reduce.py gpurun_out/r06_c3_pmct$i --match batched k_stream --prune \
                 > gpurun_out/r06_c3_pmct$i.json || return $?
             done ;;
-    stagep) timeout -k 10 1000 python -u bench.py --stage p > gpurun_out/r06_stage_p.jsonl 2> gpurun_out/r06_stage_p.err ;;
+    stagep) timeout -k 10 1000 python -u bench.py --stage p > gpurun_out/r06_stage_p${RUN:-}.jsonl 2> gpurun_out/r06_stage_p.err ;;
     stagepq) timeout -k 10 600 python -u bench.py --stage p --no-cpu-baseline > gpurun_out/r06_stage_pq.jsonl 2> gpurun_out/r06_stage_pq.err ;;
     profp)  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/r06_prof_p -o run --output-format csv \
               -- python3 bench.py --stage p --no-cpu-baseline > gpurun_out/r06_prof_p.log 2>&1 ;;
