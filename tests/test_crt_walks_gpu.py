@@ -119,7 +119,9 @@ def test_extreme_plaintexts(efl, owner):
 
 
 @pytest.mark.parametrize("tail", [0, 1, 2, 4, 8, 16])
-@pytest.mark.parametrize("n", [1, 17, 65, 2048, 32769, 100352, 100352 + 5 * 64 + 3])
+# tails of 1 to 2,371 elements (S = 16 or 8 in mode 0), 8,192 (S = 4), 16,384 (S = 2) and 17,408
+# (no split: every wave whole) past 32,768 elements (the whole rounds of 1,024 SIMDs)
+@pytest.mark.parametrize("n", [1, 17, 65, 2048, 32769, 40960, 49152, 50176, 100352, 100352 + 5 * 64 + 3])
 def test_tree_tail_equals_per_key(efl, owner, tail, n):
     """The tail past the whole rounds as a product tree across lanes, in the whole rounds' launch
     (efl_pl_tune(ln, 6, 0), the default) or after it (2-16, a fixed S), or as the round-5
