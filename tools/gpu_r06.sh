@@ -93,6 +93,11 @@ run() {
                 > gpurun_out/r06_mask_pmc_$c.json || return $?
             done ;;
     masklay) timeout -k 10 300 python -u tools/mask_layout_probe.py ${MASKLAY_ARGS:-} >> gpurun_out/r06_mask_layout.jsonl 2> gpurun_out/r06_mask_layout.err ;;
+    layer)  timeout -k 10 400 python -u tools/bench_layer.py --steps 3 --warmup 1 > gpurun_out/r06_layer_dense.jsonl 2> gpurun_out/r06_layer_dense.err && \
+            timeout -k 10 400 python -u tools/bench_layer.py --steps 3 --warmup 1 --kind weight > gpurun_out/r06_layer_weight.jsonl 2> gpurun_out/r06_layer_weight.err ;;
+    spillpmc) timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_FLAT SQ_ACTIVE_INST_FLAT SQ_WAVE_CYCLES SQ_INSTS \
+              -d gpurun_out/r06_spill_pmc -o run --output-format csv \
+              -- python3 tools/spill_probe.py > gpurun_out/r06_spill_pmc.log 2>&1 ;;
     crtprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r06_crt_prof -o run --output-format csv \
               -- python3 tools/crt_tail_ab.py --modes 1,16,8 --rounds 2 > gpurun_out/r06_crt_prof.log 2>&1 ;;
     crtab)  timeout -k 10 400 python -u tools/crt_tail_ab.py >> gpurun_out/r06_crt_tail_ab.jsonl 2> gpurun_out/r06_crt_tail_ab.err ;;
