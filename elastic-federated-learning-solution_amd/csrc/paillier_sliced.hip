@@ -1403,6 +1403,9 @@ __device__ __forceinline__ void m_func(uint32_t (&res)[C / 2], const uint32_t* _
   // otherwise (the short-slice families keep CIOS: their unrolled folded loops cost compile time
   // for little)
   constexpr bool kFold = G > 1 && C == 32 && EFL_SQR_FOLD;
+  // SOS squarings for the 37-limb slices over 2 or 4 lanes (the 2048- and 4096-bit keys' defaults)
+  // when the sliding window's table slab is there (the binary method keeps CIOS)
+  constexpr bool kSos = !kFold && (G == 2 || G == 4) && C == 32 && EFL_SQR_SOS;
   const uint32_t minv28 = second ? k.d.q2_minv28 : k.d.p2_minv28;
   const uint32_t* r2_28 = k.at(second ? k.d.off_q2_r2_28[kLog2G] : k.d.off_p2_r2_28[kLog2G]);
   const uint32_t* m28_at = k.at(second ? k.d.off_q2_28 : k.d.off_p2_28);
@@ -1490,6 +1493,86 @@ __device__ __forceinline__ void m_func(uint32_t (&res)[C / 2], const uint32_t* _
     s28::mont_mul_folded<C28, G>(a, Unit{}, BASE, E, m28, minv28, g);   // y = c^(x-1) mod x^2
     lds_sync();
     s28::to_lds_folded<C28, G>(SCR, E, g, a);
+    lds_sync();
+  } else if constexpr (kSos) {
+    // the SOS squarings (sliced28.h sos_sqr) take both LDS arrays as the square's 2 L words; one
+    // call site for every squaring of the window walk (its code is about 3,500 instructions)
+    uint32_t a[C28], m28[C28];
+    s28::from_words<C28>(a, SCR, E, L, g);
+    slice_uniform<C28>(m28, m28_at, g);
+    s28::mont_mul<C28, G>(a, Uniform{r2_28}, m28, minv28, g);
+    lds_sync();
+    if (!tab) {                                    // the binary method (efl_pl_tune(ln, 2, 0)): CIOS
+      to_lds<C28>(BASE, E, g, a);
+#pragma unroll 1
+      for (int b = ebits - 2; b >= 0; --b) {
+        s28::mont_sqr<C28, G>(a, SCR, E, m28, minv28, g);
+        if (ebit(ex, b)) s28::mont_mul<C28, G>(a, LdsElem{BASE, E}, m28, minv28, g);
+      }
+    } else {
+    constexpr int CP = pad4<C28>();
+    uint32_t* slot = tab + g * CP;                 // entry e at slot + e * G * CP
+    store28<C28>(slot, a);
+    int b = ebits - 1;
+    int j = b - kDecWin + 1 > 0 ? b - kDecWin + 1 : 0;
+    while (!ebit(ex, j)) ++j;
+    uint32_t v = 0;
+    for (int t = b; t >= j; --t) v = (v << 1) | ebit(ex, t);
+    // phase -1: c^2, then the odd powers; phase 0: the window walk
+    int nsq = 1;
+    int e2 = 0;                                    // table entries built so far (after c^2)
+    bool build = true;
+    size_t ent_at = 0;
+    bool mul = false;
+#pragma unroll 1
+    for (;;) {
+#pragma unroll 1
+      for (int t = 0; t < nsq; ++t) {
+        s28::sos_sqr<C28, G>(a, BASE, E, m28, minv28, g);
+        lds_sync();
+      }
+      if (build) {
+        // a = c^2: stage it, then T[e] = T[e-1] c^2 from c
+        to_lds<C28>(BASE, E, g, a);
+        lds_sync();
+        load28<C28>(a, slot);
+#pragma unroll 1
+        for (e2 = 1; e2 < kDecEntries; ++e2) {
+          s28::mont_mul<C28, G>(a, LdsElem{BASE, E}, m28, minv28, g);
+          store28<C28>(slot + (size_t)e2 * G * CP, a);
+        }
+        lds_sync();
+        load28<C28>(a, slot + (size_t)(v >> 1) * G * CP);
+        b = j - 1;
+        build = false;
+      } else if (mul) {
+        uint32_t ent[C28];
+        load28<C28>(ent, slot + ent_at);
+        to_lds<C28>(BASE, E, g, ent);
+        lds_sync();
+        s28::mont_mul<C28, G>(a, LdsElem{BASE, E}, m28, minv28, g);
+        lds_sync();
+      }
+      if (b < 0) break;
+      if (!ebit(ex, b)) {
+        nsq = 1;
+        mul = false;
+        --b;
+      } else {
+        j = b - kDecWin + 1 > 0 ? b - kDecWin + 1 : 0;
+        while (!ebit(ex, j)) ++j;
+        v = 0;
+        for (int t = b; t >= j; --t) v = (v << 1) | ebit(ex, t);
+        ent_at = (size_t)(v >> 1) * G * CP;
+        nsq = b - j + 1;
+        mul = true;
+        b = j - 1;
+      }
+    }
+    }
+    s28::mont_mul<C28, G>(a, Unit{}, m28, minv28, g);   // y = c^(x-1) mod x^2
+    lds_sync();
+    to_lds<C28>(SCR, E, g, a);
     lds_sync();
   } else {
   uint32_t a[C28], m28[C28];

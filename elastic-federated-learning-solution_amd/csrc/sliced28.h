@@ -38,6 +38,11 @@ namespace s28 {
 #ifndef EFL_SQR_FOLD
 #define EFL_SQR_FOLD 0
 #endif
+// Decryption squarings of numbers over G = 2 or 4 lanes by separated operand scanning (round 6,
+// sos_sqr; build knob for A/B: EFL_SQR_SOS=0 builds the blocked CIOS squaring)
+#ifndef EFL_SQR_SOS
+#define EFL_SQR_SOS 1
+#endif
 // One-lane squarings by product scanning (sqr_fips1) instead of CIOS through LDS (build knob for
 // A/B: EFL_SQR_FIPS=0 builds the round-2 squaring)
 #ifndef EFL_SQR_FIPS
@@ -521,6 +526,153 @@ __device__ __forceinline__ void to_words(uint32_t (&w)[C32], const uint32_t* l28
   }
 }
 
+
+// ---- separated operand scanning squaring (round 6; the G = 2 / 4 decryption families) -------------
+// a^2 R^-1 mod m for a number over G lanes (lane g: limbs g C .. g C + C - 1), in two phases.
+// Phase 1 forms the square a^2 (2 L limbs) in the element's LDS words T (the decryption's two LDS
+// arrays, contiguous: T[p] at T0[p * E]) as sub-products scanned by columns in registers, each
+// column's 28-bit limb added with ds_add_u32. Lane g takes A_g^2 (symmetric: C (C + 1) / 2 products),
+// the full cross product 2 A_g A_(g+1 mod G) (G = 4), and half the rows of one more cross pair (G = 4:
+// the distance-2 pairs (0, 2), (1, 3); G = 2: the one pair (0, 1)), the partner chunks taken by
+// DPP lane rotations: C (C + 1) / 2 + C^2 + C H products per lane at G = 4 (2,812 at C = 37) against
+// CIOS's 2 L C = 10,952 for the whole product. Phase 2 is the reduction alone: L CIOS steps of
+// C products m u over the lane-sliced window holding the low half, and then the high half added.
+// Bounds: a column holds at most C products < 2^57 (cross rows doubled) and a carry < 2^36; a T word
+// at most 7 limbs < 2^29 (< 2^32); the window adds < 2^56 per step, lazily normalised every 64
+// steps, and stays < R. Output <= 2m for input <= 2m (R > 4m), which later products accept.
+// tools/sos_sim.py simulates the same steps lane by lane against (x^2 + U m) / R.
+
+// lane g <- lane (g + D) mod G inside aligned groups (G = 2: D = 1; G = 4: D = 1, 2)
+template <int G, int D>
+__device__ __forceinline__ uint32_t rot_lane(uint32_t v) {
+  static_assert(G == 2 || G == 4, "rotations for pairs and quads");
+  if constexpr (G == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // [1,0,3,2]
+  else if constexpr (D == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x39, 0xF, 0xF, false);  // [1,2,3,0]
+  else return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);   // [2,3,0,1]
+}
+
+// x (R rows) times y (C limbs) by columns; COLS column limbs added to T[k * E] (the last takes the
+// rest of the carry). A template recursion over the column K, so every column's row range and every
+// register index is a compile-time constant (a loop nest with run-time bounds went to scratch)
+template <int R, int C, int COLS, int K>
+__device__ __forceinline__ void scan_col(const uint32_t (&x)[R], const uint32_t (&y)[C], uint32_t* T, int E,
+                                         uint64_t carry) {
+  if constexpr (K < COLS) {
+    constexpr int rlo = K - C + 1 > 0 ? K - C + 1 : 0;
+    constexpr int rhi = K < R - 1 ? K : R - 1;
+    uint64_t x0 = carry, x1 = 0;
+#pragma unroll
+    for (int r = rlo; r <= rhi; ++r) {
+      if ((r - rlo) & 1) x1 = (uint64_t)x[r] * y[K - r] + x1;
+      else x0 = (uint64_t)x[r] * y[K - r] + x0;
+    }
+    const uint64_t acc = x0 + x1;
+    if constexpr (K < COLS - 1) {
+      atomicAdd(&T[K * E], (uint32_t)acc & kMask);
+      scan_col<R, C, COLS, K + 1>(x, y, T, E, acc >> kBits);
+    } else {
+      atomicAdd(&T[K * E], (uint32_t)acc);
+    }
+  }
+}
+template <int R, int C, int COLS>
+__device__ __forceinline__ void scan_add(const uint32_t (&x)[R], const uint32_t (&y)[C], uint32_t* T, int E) {
+  scan_col<R, C, COLS, 0>(x, y, T, E, 0);
+}
+
+// a^2 by columns (each cross product once, doubled), 2 C column limbs added to T[k * E]
+template <int C, int K>
+__device__ __forceinline__ void sqr_col(const uint32_t (&a)[C], uint32_t* T, int E, uint64_t carry) {
+  if constexpr (K < 2 * C) {
+    constexpr int ilo = K - C + 1 > 0 ? K - C + 1 : 0;   // j = K - i < C
+    constexpr int ihi = K >= 1 ? (K - 1) / 2 : -1;        // i < j (none in column 0)
+    uint64_t x0 = 0, x1 = 0;
+#pragma unroll
+    for (int i = ilo; i <= ihi; ++i) {
+      if ((i - ilo) & 1) x1 = (uint64_t)a[i] * a[K - i] + x1;
+      else x0 = (uint64_t)a[i] * a[K - i] + x0;
+    }
+    uint64_t acc = ((x0 + x1) << 1) + carry;
+    if constexpr ((K & 1) == 0 && (K >> 1) < C) acc = (uint64_t)a[K >> 1] * a[K >> 1] + acc;
+    if constexpr (K < 2 * C - 1) {
+      atomicAdd(&T[K * E], (uint32_t)acc & kMask);
+      sqr_col<C, K + 1>(a, T, E, acc >> kBits);
+    } else {
+      atomicAdd(&T[K * E], (uint32_t)acc);
+    }
+  }
+}
+template <int C>
+__device__ __forceinline__ void sqr_scan_add(const uint32_t (&a)[C], uint32_t* T, int E) {
+  sqr_col<C, 0>(a, T, E, 0);
+}
+
+template <int C, int G>
+__device__ __forceinline__ void sos_sqr(uint32_t (&a)[C], uint32_t* T, int E, const uint32_t (&m)[C], uint32_t minv,
+                                        int g) {
+  static_assert(G == 2 || G == 4, "SOS squaring for pairs and quads of lanes");
+  constexpr int L = C * G, H = (C + 1) / 2;
+#pragma unroll
+  for (int j = 0; j < 2 * C; ++j) T[(g * 2 * C + j) * E] = 0u;
+  sl::lds_sync();
+  sqr_scan_add<C>(a, T + (2 * g * C) * E, E);
+  uint32_t y[C], x[H];
+  if constexpr (G == 4) {
+    // the full cross product with the next lane's chunk, doubled
+#pragma unroll
+    for (int j = 0; j < C; ++j) y[j] = rot_lane<G, 1>(a[j]) << 1;
+    const int off1 = (g + ((g + 1) & 3)) * C;
+    scan_add<C, C, 2 * C + 1>(a, y, T + off1 * E, E);
+    // half the rows of the distance-2 pair: g < 2 rows [0, H) of A_g against 2 A_(g+2); g >= 2 rows
+    // [H, C) of A_(g-2) against 2 A_g
+    uint32_t p2[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) p2[j] = rot_lane<G, 2>(a[j]);
+    const bool lo = g < 2;
+#pragma unroll
+    for (int r = 0; r < H; ++r) x[r] = lo ? a[r] : (H + r < C ? p2[H + r] : 0u);
+#pragma unroll
+    for (int j = 0; j < C; ++j) y[j] = (lo ? p2[j] : a[j]) << 1;
+    const int off2 = lo ? (2 * g + 2) * C : (2 * g - 2) * C + H;
+    scan_add<H, C, H + C + 1>(x, y, T + off2 * E, E);
+  } else {
+    // the one pair (0, 1): lane 0 rows [0, H) of A_0, lane 1 rows [H, C) of A_0, against 2 A_1
+    uint32_t p1[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) p1[j] = rot_lane<G, 1>(a[j]);
+    const bool lo = g == 0;
+#pragma unroll
+    for (int r = 0; r < H; ++r) x[r] = lo ? a[r] : (H + r < C ? p1[H + r] : 0u);
+#pragma unroll
+    for (int j = 0; j < C; ++j) y[j] = (lo ? p1[j] : a[j]) << 1;
+    const int off2 = lo ? C : C + H;
+    scan_add<H, C, H + C + 1>(x, y, T + off2 * E, E);
+  }
+  sl::lds_sync();
+  // phase 2: the low half's reduction over the lane-sliced window, then the high half added:
+  // (T + U m) / R = T_hi + (T_lo + U m) / R (U depends on T_lo only; the window stays < R, so the
+  // top lane takes nothing in, as in mont_mul)
+  uint64_t W[C];
+#pragma unroll
+  for (int j = 0; j < C; ++j) W[j] = T[(g * C + j) * E];
+#pragma unroll 2
+  for (int i = 0; i < L; ++i) {
+    const uint32_t u = sl::bcast0<G>(((uint32_t)W[0] * minv) & kMask);
+#pragma unroll
+    for (int j = 0; j < C; ++j) W[j] = (uint64_t)m[j] * u + W[j];
+    uint64_t in = from_next64<G>(W[0]);
+    if (g == G - 1) in = 0;
+    const uint64_t c0 = W[0] >> kBits;   // lane 0: the bottom limb is now 0 mod 2^28
+#pragma unroll
+    for (int j = 0; j < C - 1; ++j) W[j] = W[j + 1];
+    W[C - 1] = in;
+    if (g == 0) W[0] += c0;
+    if (L > 64 && (i & 63) == 63) lazy_normalize<C, G>(W, g);
+  }
+#pragma unroll
+  for (int j = 0; j < C; ++j) W[j] += T[(L + g * C + j) * E];
+  normalize<C, G>(a, W, g);
+}
 
 }  // namespace s28
 }  // namespace efl

@@ -76,6 +76,12 @@ run() {
             done ;;
     dect)   timeout -k 10 900 $PT tests/test_paillier_gpu.py tests/test_paillier_key_sizes_gpu.py -k "decrypt or round_trip" \
               > gpurun_out/r06_dec_tests.log 2>&1 ;;
+    decsos) for r in 1 2; do
+              for v in "" _ship; do
+                EFL_HIP_LIB=$LIBDIR/libefl_hip$v.so timeout -k 10 300 python -u tools/dec_ab.py --label "lib$v" \
+                  >> gpurun_out/r06_dec_sos.jsonl 2>> gpurun_out/r06_dec_sos.err || return $?
+              done
+            done ;;
     decpmc) for v in _fold _nofold; do
               EFL_HIP_LIB=$LIBDIR/libefl_hip$v.so timeout -s KILL 150 rocprofv3 \
                 --pmc SQC_ICACHE_MISSES SQC_ICACHE_HITS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_WAVES \
